@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json's metric: CRC32C GB/s (device-resident) over
+2^20 x 1400 B datagrams, bit-exact.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fixed|csr]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+A step is one launch of the batched CRC-32C kernel over the rank's resident
+shard (config 2: 2^20 x 1400 B per GPU at stride 1400; config 4 = the same per
+GPU at N = 8: weak scaling, packets sharded by contiguous ranges, no
+collective on the data path -- the only collectives are the timing barrier and
+a MAX over per-rank times).  Inputs are generated on the device before the
+timed region.  Rank 0 prints ONE JSON line.
+
+roofline: algorithmic bytes per launch = sum(L) + 4 N (datagram bytes read +
+CRC words written; CSR adds 8 N offset bytes) over the average kernel time
+measured with HIP events on the launch stream; peak 8.0 TB/s (MI355X HBM3E
+nameplate).  traffic: HBM bytes per launch from the rocprofv3 PMC pass
+(profiles/traffic_<workload>.json, FETCH_SIZE x2 gfx950 correction +
+WRITE_SIZE) when present, else null.
+cpu_baseline: the oracle's batch CRC (SSE4.2 crc32 instruction, OpenMP) timed
+on this host's cores over a bounded sample of the same batch (rank 0, N = 1).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E nameplate, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "CRC32C GB/s (device-resident) over 1M×1400B packets; bit-exact"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["fixed", "csr"], default="fixed")
+    ap.add_argument("--packets", type=int, default=1 << 20, help="per GPU")
+    ap.add_argument("--length", type=int, default=1400)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time lnl_crc32c_batch_host (PCIe-inclusive, config 5)")
+    return ap.parse_args()
+
+
+def make_workload(args, rank, device):
+    """Device-resident synthetic batch (generated on the GPU, untimed)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(42 + rank)
+    n = args.packets
+    if args.workload == "fixed":
+        L = args.length
+        data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
+        return dict(data=data, n=n, L=L, off=None, payload=n * L, algo=n * L + 4 * n)
+    # config 3: lengths 64 + U[0, 1337), packed CSR with int64 offsets
+    lens = torch.randint(64, 1401, (n,), dtype=torch.int64, device=device, generator=g)
+    off = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    off[1:] = torch.cumsum(lens, 0)
+    total = int(off[-1].item())
+    data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=device, generator=g)
+    return dict(data=data, n=n, L=None, off=off, payload=total, algo=total + 4 * n + 8 * (n + 1))
+
+
+def launch(P, w, out, stream):
+    if w["off"] is None:
+        P.batch_fixed(w["data"], w["L"], w["L"], w["n"], out=out, stream=stream)
+    else:
+        P.batch_csr(w["data"], w["off"], out=out, stream=stream)
+
+
+def hbm_probe_peak(data, device):
+    """Measured read-only streaming rate over the same buffer (context for the
+    nameplate peak)."""
+    so = os.path.join(ROOT, "litenetlibpp_amd", "libhbm_probe.so")
+    if not os.path.exists(so):
+        return None
+    L = ctypes.CDLL(so)
+    L.lnl_probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    sink = torch.zeros(4, dtype=torch.int32, device=device)
+    s = torch.cuda.current_stream()
+    nbytes = data.numel() // 16 * 16
+    for _ in range(3):
+        L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream)
+    e1.record()
+    torch.cuda.synchronize()
+    return nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+
+def cpu_baseline(w, gpu_out):
+    """Oracle batch CRC on this host over a bounded sample of the same batch;
+    also checks the GPU output on that sample (bit-exact)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle
+    n_s = min(w["n"], 1 << 17)
+    if w["off"] is None:
+        L = w["L"]
+        sample = w["data"][: n_s * L].cpu().numpy()
+        def run(th):
+            return oracle.batch_fixed(sample, L, L, n_s, threads=th)
+        sbytes = n_s * L
+        desc = f"{n_s} x {L} B datagrams (first {sbytes / 1e6:.1f} MB of the GPU batch)"
+    else:
+        off = w["off"][: n_s + 1].cpu().numpy().astype(np.uint64)
+        sample = w["data"][: int(off[-1])].cpu().numpy()
+        def run(th):
+            return oracle.batch_csr(sample, off, threads=th)
+        sbytes = int(off[-1] - off[0])
+        desc = f"first {n_s} mixed-length datagrams ({sbytes / 1e6:.1f} MB) of the GPU batch"
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    res = {}
+    for th in (1, threads):
+        best, ref = None, None
+        t_end = time.perf_counter() + 3.0
+        while True:
+            t0 = time.perf_counter()
+            ref = run(th)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+            if time.perf_counter() > t_end:
+                break
+        res[th] = (sbytes / best / 1e9, ref)
+    exact = bool(np.array_equal(gpu_out[:n_s], res[threads][1]))
+    return res, threads, desc, exact
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    import litenetlibpp_amd as P
+    P.lib()
+
+    w = make_workload(args, rank, device)
+    out = torch.empty(w["n"], dtype=torch.int32, device=device)
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        launch(P, w, out, stream)
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        launch(P, w, out, stream)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    wall = t1 - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if world > 1:
+        tt = torch.tensor([wall], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+        kt = torch.tensor([kern_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+        kern_ms = float(kt.item())
+
+    ms_per_step = wall / args.steps * 1e3
+    total_payload = w["payload"] * world  # identical shard sizes (fixed); csr: rank-0 estimate
+    if w["off"] is not None and world > 1:
+        tp = torch.tensor([w["payload"]], dtype=torch.float64, device=device)
+        dist.all_reduce(tp)
+        total_payload = float(tp.item())
+    value = total_payload / (ms_per_step * 1e-3) / 1e9
+    achieved = w["algo"] / (kern_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        line = {
+            "metric": METRIC if args.workload == "fixed" else "CRC32C GB/s (device-resident) over 1M mixed-length (64-1400B) packets; bit-exact",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randint on device, seed 42+rank), resident in HBM before timing",
+            "config": {
+                "workload": ("config2: 2^20 x 1400 B datagrams per GPU, fixed stride 1400, device-resident"
+                             if args.workload == "fixed" else
+                             "config3: 2^20 mixed-length datagrams (64..1400 B uniform) per GPU, CSR int64 offsets"),
+                "packets_per_gpu": w["n"],
+                "payload_bytes_per_gpu": w["payload"],
+                "parallelism": f"shard{world} (contiguous packet ranges, no data-path collectives)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": w["algo"],
+                "kernel_ms": round(kern_ms, 5),
+            },
+        }
+        probe = hbm_probe_peak(w["data"], device)
+        if probe:
+            line["roofline"]["measured_stream_read_peak_gbs"] = round(probe, 1)
+        if world == 1 and not args.no_cpu_baseline:
+            gpu_out = out.cpu().numpy().view(np.uint32)
+            res, threads, desc, exact = cpu_baseline(w, gpu_out)
+            line["cpu_baseline"] = {
+                "value": round(res[threads][0], 3),
+                "unit": "GB/s",
+                "cores": threads,
+                "kind": "port",
+                "sample": desc + f"; oracle SSE4.2 crc32 loop, OpenMP {threads} threads, best of repeats over ~3 s",
+                "single_core_value": round(res[1][0], 3),
+            }
+            line["parity_on_sample"] = "bit-exact" if exact else "MISMATCH"
+        if args.host_path and world == 1:
+            line["host_path"] = host_path_rate(P, w)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def host_path_rate(P, w):
+    """Config 5: host-resident pinned batch -> lnl_crc32c_batch_host (H2D +
+    kernel + D2H over 2 streams).  PCIe-inclusive; never the headline value."""
+    if w["off"] is None:
+        n, L = w["n"], w["L"]
+        host = w["data"].cpu().pin_memory()
+        off = np.arange(0, (n + 1) * L, L, dtype=np.uint64)
+    else:
+        host = w["data"].cpu().pin_memory()
+        off = w["off"].cpu().numpy().astype(np.uint64)
+    arr = host.numpy()
+    P.batch_host(arr, off, torch.cuda.current_device())
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        P.batch_host(arr, off, torch.cuda.current_device())
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(w["payload"] / dt / 1e9, 2), "unit": "GB/s",
+            "what": "pinned host batch, lnl_crc32c_batch_host, H2D+kernel+D2H, 2 streams"}
+
+
+if __name__ == "__main__":
+    main()

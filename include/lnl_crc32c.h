@@ -1,0 +1,117 @@
+/*
+ * lnl_crc32c.h -- C ABI of the MI355X-native CRC-32C packet-layer path.
+ *
+ * Drop-in boundary.  The reference (Revan600/LiteNetLibPP) has no packet
+ * layers and no checksum (/root/reference/README.MD:35); its upstream C#
+ * original exposes CRC-32C as a PacketLayerBase subclass
+ * (ExtraPacketSizeForLayer = 4, ProcessOutBoundPacket, ProcessInboundPacket).
+ * These entry points are what a net_manager would bind at its two datagram
+ * choke points:
+ *
+ *   outbound  net_manager::send_raw, before sendto
+ *             /root/reference/src/lnl/net_manager.cpp:515-523
+ *   inbound   net_manager::receive_logic, after recvfrom + packet->resize and
+ *             before on_message_received / packet->verify()
+ *             /root/reference/src/lnl/net_manager.cpp:210-222, :342-343
+ *
+ * over the bytes net_packet::data()[0 .. size())
+ * (/root/reference/include/lnl/net_packet.h:112-118), with every MTU of
+ * net_constants::POSSIBLE_MTU (/root/reference/include/lnl/net_constants.h:29-39)
+ * reduced by LNL_CRC32C_LAYER_EXTRA when the layer is on.
+ *
+ * CRC-32C: Castagnoli, reflected polynomial 0x82F63B78, init and xorout
+ * 0xFFFFFFFF; CRC("123456789") = 0xE3069283; CRC of 0 bytes = 0.
+ *
+ * Conventions
+ *   - Callers own every buffer.  d_* pointers are device memory of the
+ *     current HIP device; h_* pointers are host memory.
+ *   - *_dev calls are asynchronous and ordered on `hip_stream` (a hipStream_t,
+ *     NULL = the null stream).  They never synchronise.  *_host calls block.
+ *   - Return 0 on success or a negative errno-style code:
+ *       -EINVAL (-22) bad argument, -ENODEV (-19) no usable gfx950 device,
+ *       -ENOMEM (-12) allocation failure, -EIO (-5) a HIP runtime error.
+ *     lnl_crc32c_last_error() returns this thread's message for the last
+ *     failure.  No C++ exception crosses this ABI.
+ *   - Empty batches (n == 0) are valid and launch nothing.
+ *   - No batch entry point ever computes on the CPU: without a usable GPU
+ *     they fail with -ENODEV.
+ */
+#ifndef LNL_CRC32C_H
+#define LNL_CRC32C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LNL_CRC32C_ABI_VERSION 1
+
+/* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
+#define LNL_CRC32C_LAYER_EXTRA 4
+
+/* ---- per-datagram CPU path (send_raw / receive_logic hooks) -------------- */
+
+/* CRC-32C of p[0..n).  Stateless, reentrant, thread-safe: send_raw runs on the
+ * receive, logic and user threads (/root/reference/src/lnl/net_manager.cpp:106-107).
+ * Uses the SSE4.2 crc32 instruction when the host has it. */
+uint32_t lnl_crc32c(const uint8_t* p, size_t n);
+
+/* Incremental form: lnl_crc32c_extend(lnl_crc32c(a), b) == lnl_crc32c(a || b);
+ * lnl_crc32c_extend(0, p, n) == lnl_crc32c(p, n). */
+uint32_t lnl_crc32c_extend(uint32_t crc, const uint8_t* p, size_t n);
+
+/* Outbound layer step (upstream Crc32cLayer.ProcessOutBoundPacket): writes
+ * data[offset .. offset+length) followed by LE32(crc32c of those bytes) into
+ * dst (dst may not alias data; data is const and may be a shared per-peer
+ * buffer, see /root/reference/src/lnl/net_peer.cpp:482, :575).  Returns the
+ * new length (length + 4) or a negative code if dst_cap is too small. */
+int64_t lnl_crc32c_layer_outbound(const uint8_t* data, size_t offset, size_t length,
+                                  uint8_t* dst, size_t dst_cap);
+
+/* Inbound layer step (upstream Crc32cLayer.ProcessInboundPacket): returns the
+ * payload length (length - 4) if length >= 5 and the trailing LE32 matches the
+ * CRC-32C of the preceding bytes, else -1 (drop silently: a checksum failure
+ * looks like packet loss to the reliability layer). */
+int64_t lnl_crc32c_layer_inbound(const uint8_t* data, size_t length);
+
+/* ---- batched GPU path (gfx950 kernels) ----------------------------------- */
+
+/* out[i] = CRC32C(d_base + i*stride, len), i < n.  stride >= len. */
+int lnl_crc32c_batch_fixed_dev(const uint8_t* d_base, size_t stride, uint32_t len,
+                               uint32_t n, uint32_t* d_out, void* hip_stream);
+
+/* out[i] = CRC32C(d_base + d_off[i], d_off[i+1] - d_off[i]), i < n.
+ * d_off holds n+1 non-decreasing byte offsets; any byte alignment. */
+int lnl_crc32c_batch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                             uint32_t* d_out, void* hip_stream);
+
+/* Batched inbound verification (the layer's receive side over a CSR batch of
+ * whole datagrams, trailing LE32 CRC included): d_ok[i] = 1 if datagram i has
+ * length >= 5 and its trailing CRC matches, else 0.  d_crc (optional, may be
+ * NULL) receives the CRC computed over the first length-4 bytes. */
+int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                              uint8_t* d_ok, uint32_t* d_crc, void* hip_stream);
+
+/* Host-resident batch (the socket path): copies h_base/h_off to `device`
+ * in chunks over two HIP streams (H2D -> kernel -> D2H overlapped), writes
+ * h_out[i], blocks until done.  h_off as in batch_csr_dev (h_off[0] may be
+ * nonzero).  Pinned (hipHostMalloc / hipHostRegister) buffers give the full
+ * PCIe rate; pageable ones work but copy through a staging buffer. */
+int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
+                          uint32_t* h_out, int device);
+
+/* ---- misc ---------------------------------------------------------------- */
+
+/* Message for the last failure on the calling thread ("" if none). */
+const char* lnl_crc32c_last_error(void);
+
+/* LNL_CRC32C_ABI_VERSION of the loaded library. */
+int lnl_crc32c_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LNL_CRC32C_H */

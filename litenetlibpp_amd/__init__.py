@@ -1,0 +1,21 @@
+"""litenetlibpp_amd -- MI355X-native CRC-32C packet-layer path for a
+LiteNetLibPP-style reliable-UDP stack.
+
+The product is ``liblnl_crc32c.so`` (gfx950 HIP kernels + a C ABI,
+``include/lnl_crc32c.h``); this package is its Python mirror.
+"""
+from .crc32c import (  # noqa: F401
+    EXTRA_PACKET_SIZE,
+    Crc32cError,
+    Crc32cLayer,
+    batch_csr,
+    batch_fixed,
+    batch_host,
+    crc32c,
+    crc32c_extend,
+    mtu_with_layer,
+    verify_csr,
+)
+from ._lib import LIB_PATH, lib  # noqa: F401
+
+__version__ = "0.1.0"

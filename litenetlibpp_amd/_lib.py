@@ -1,0 +1,70 @@
+"""ctypes binding of the in-tree product library ``liblnl_crc32c.so``.
+
+This is the Python mirror of the C ABI in ``include/lnl_crc32c.h`` (the same
+entry points a cgo/JNI/ctypes maintainer would bind).  It
+loads ONLY the in-tree library and raises if it is missing: there is no
+Python or CPU fallback for the batch entry points.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblnl_crc32c.so")
+
+_c_u8p = ctypes.c_void_p  # raw addresses (host bytes or device pointers)
+
+
+class Crc32cError(RuntimeError):
+    """A negative return code from the C ABI (errno-style) plus its message."""
+
+    def __init__(self, code: int, what: str, msg: str):
+        super().__init__(f"{what} failed ({code}): {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+            "or `make -C litenetlibpp_amd` (no fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.lnl_crc32c.restype = ctypes.c_uint32
+    L.lnl_crc32c.argtypes = [_c_u8p, ctypes.c_size_t]
+    L.lnl_crc32c_extend.restype = ctypes.c_uint32
+    L.lnl_crc32c_extend.argtypes = [ctypes.c_uint32, _c_u8p, ctypes.c_size_t]
+    L.lnl_crc32c_layer_outbound.restype = ctypes.c_int64
+    L.lnl_crc32c_layer_outbound.argtypes = [_c_u8p, ctypes.c_size_t, ctypes.c_size_t, _c_u8p,
+                                            ctypes.c_size_t]
+    L.lnl_crc32c_layer_inbound.restype = ctypes.c_int64
+    L.lnl_crc32c_layer_inbound.argtypes = [_c_u8p, ctypes.c_size_t]
+    L.lnl_crc32c_batch_fixed_dev.restype = ctypes.c_int
+    L.lnl_crc32c_batch_fixed_dev.argtypes = [_c_u8p, ctypes.c_size_t, ctypes.c_uint32,
+                                             ctypes.c_uint32, _c_u8p, ctypes.c_void_p]
+    L.lnl_crc32c_batch_csr_dev.restype = ctypes.c_int
+    L.lnl_crc32c_batch_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p,
+                                           ctypes.c_void_p]
+    L.lnl_crc32c_verify_csr_dev.restype = ctypes.c_int
+    L.lnl_crc32c_verify_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p,
+                                            ctypes.c_void_p]
+    L.lnl_crc32c_batch_host.restype = ctypes.c_int
+    L.lnl_crc32c_batch_host.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, ctypes.c_int]
+    L.lnl_crc32c_last_error.restype = ctypes.c_char_p
+    L.lnl_crc32c_last_error.argtypes = []
+    L.lnl_crc32c_abi_version.restype = ctypes.c_int
+    L.lnl_crc32c_abi_version.argtypes = []
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().lnl_crc32c_last_error().decode(errors="replace")
+        raise Crc32cError(rc, what, msg)

@@ -1,0 +1,194 @@
+"""Host-side mirror of the CRC-32C packet-layer path.
+
+Two halves, both thin wrappers over the C ABI (include/lnl_crc32c.h):
+
+* per-datagram (CPU, product code in csrc/crc32c_host.cpp): ``crc32c``,
+  ``crc32c_extend`` and ``Crc32cLayer`` -- the packet layer the reference's
+  ``net_manager`` would call at its two datagram choke points
+  (/root/reference/src/lnl/net_manager.cpp:515-523 outbound before ``sendto``;
+  :210-222 inbound after ``recvfrom``/``resize``, before ``verify()`` at :343).
+  It mirrors upstream LiteNetLib's ``Crc32cLayer``: 4 extra bytes per datagram,
+  append LE32(crc) outbound, drop silently inbound when the datagram is shorter
+  than header + CRC or the CRC does not match.
+* batched (gfx950 kernels): ``batch_fixed``, ``batch_csr``, ``verify_csr`` on
+  device tensors, ``batch_host`` on host buffers.  These never compute on the
+  CPU; without the library or a gfx950 GPU they raise.
+
+Device buffers are torch tensors (torch is plumbing here: device memory and
+streams).  CRC results are returned as ``torch.int32`` tensors holding the
+uint32 bit patterns (use ``.cpu().numpy().view(np.uint32)``).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from ._lib import Crc32cError, check, lib
+
+EXTRA_PACKET_SIZE = 4  # LNL_CRC32C_LAYER_EXTRA / upstream ExtraPacketSizeForLayer
+HEADER_SIZE = 1        # net_constants::HEADER_SIZE (/root/reference/include/lnl/net_constants.h:16)
+
+__all__ = [
+    "Crc32cError", "EXTRA_PACKET_SIZE", "crc32c", "crc32c_extend", "Crc32cLayer",
+    "batch_fixed", "batch_csr", "verify_csr", "batch_host", "mtu_with_layer",
+]
+
+
+def _addr(buf) -> tuple[int, int, object]:
+    """(address, length, keepalive) of a bytes-like or numpy buffer."""
+    if isinstance(buf, np.ndarray):
+        if not buf.flags["C_CONTIGUOUS"]:
+            buf = np.ascontiguousarray(buf)
+        return buf.ctypes.data, buf.nbytes, buf
+    mv = memoryview(buf).cast("B")
+    if mv.readonly:
+        arr = np.frombuffer(mv, dtype=np.uint8)
+        return arr.ctypes.data, arr.nbytes, arr
+    c = (ctypes.c_uint8 * len(mv)).from_buffer(mv)
+    return ctypes.addressof(c), len(mv), c
+
+
+# ---------------------------------------------------------------- CPU path
+def crc32c(data) -> int:
+    """CRC-32C of a bytes-like object (CRC('123456789') = 0xE3069283)."""
+    a, n, _k = _addr(data)
+    return int(lib().lnl_crc32c(a, n))
+
+
+def crc32c_extend(crc: int, data) -> int:
+    """crc32c_extend(crc32c(a), b) == crc32c(a + b)."""
+    a, n, _k = _addr(data)
+    return int(lib().lnl_crc32c_extend(crc & 0xFFFFFFFF, a, n))
+
+
+def mtu_with_layer(mtu: int) -> int:
+    """Effective MTU with the CRC layer on: every POSSIBLE_MTU entry loses 4
+    bytes (/root/reference/include/lnl/net_constants.h:29-39)."""
+    return mtu - EXTRA_PACKET_SIZE
+
+
+class Crc32cLayer:
+    """Packet layer with upstream ``PacketLayerBase`` semantics.
+
+    ``process_outbound(data, offset, length)`` returns the bytes to hand to
+    ``sendto`` (payload + LE32 CRC) without touching ``data`` (send_raw's buffer
+    is const and may be shared, /root/reference/src/lnl/net_peer.cpp:482).
+    ``process_inbound(datagram)`` returns the payload with the CRC stripped, or
+    None to drop the datagram (it then looks like loss to the reliable channel).
+    """
+
+    extra_packet_size = EXTRA_PACKET_SIZE
+
+    def __init__(self):
+        self.dropped = 0  # "checksum: bad" counter (upstream logs it)
+
+    def process_outbound(self, data, offset: int = 0, length: Optional[int] = None) -> bytes:
+        a, n, _k = _addr(data)
+        if length is None:
+            length = n - offset
+        if offset < 0 or length < 0 or offset + length > n:
+            raise ValueError("offset/length outside data")
+        out = ctypes.create_string_buffer(length + EXTRA_PACKET_SIZE)
+        r = lib().lnl_crc32c_layer_outbound(a, offset, length, ctypes.addressof(out), len(out))
+        if r < 0:
+            raise Crc32cError(int(r), "lnl_crc32c_layer_outbound", "bad arguments")
+        return out.raw[:r]
+
+    def process_inbound(self, datagram) -> Optional[bytes]:
+        a, n, _k = _addr(datagram)
+        r = lib().lnl_crc32c_layer_inbound(a, n)
+        if r < 0:
+            self.dropped += 1
+            return None
+        return bytes(memoryview(datagram).cast("B")[:r])
+
+
+# ---------------------------------------------------------------- GPU path
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_handle(stream) -> int:
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)
+
+
+def _check_dev_u8(t, name):
+    torch = _torch()
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous()):
+        raise TypeError(f"{name} must be a contiguous torch.uint8 CUDA tensor")
+
+
+def _out_u32(out, n, device):
+    torch = _torch()
+    if out is None:
+        return torch.empty(n, dtype=torch.int32, device=device)
+    if not (out.is_cuda and out.dtype in (torch.int32, torch.uint32) and out.is_contiguous()
+            and out.numel() >= n):
+        raise TypeError("out must be a contiguous int32/uint32 CUDA tensor with >= n elements")
+    return out
+
+
+def batch_fixed(data, stride: int, length: int, n: int, out=None, stream=None):
+    """out[i] = CRC32C(data[i*stride : i*stride + length]) on the GPU."""
+    _check_dev_u8(data, "data")
+    if n < 0 or length < 0 or stride < 0:
+        raise ValueError("negative size")
+    if n and (n - 1) * stride + length > data.numel():
+        raise ValueError("batch exceeds data")
+    out = _out_u32(out, n, data.device)
+    check(lib().lnl_crc32c_batch_fixed_dev(data.data_ptr(), stride, length, n, out.data_ptr(),
+                                           _stream_handle(stream)), "lnl_crc32c_batch_fixed_dev")
+    return out
+
+
+def _check_off(offsets, data):
+    torch = _torch()
+    if not (offsets.is_cuda and offsets.dtype in (torch.int64, torch.uint64) and offsets.is_contiguous()):
+        raise TypeError("offsets must be a contiguous int64 CUDA tensor (n + 1 entries)")
+
+
+def batch_csr(data, offsets, out=None, stream=None):
+    """out[i] = CRC32C(data[off[i]:off[i+1]]) on the GPU (offsets: n+1 int64)."""
+    _check_dev_u8(data, "data")
+    _check_off(offsets, data)
+    n = offsets.numel() - 1
+    out = _out_u32(out, max(n, 0), data.device)
+    if n > 0:
+        check(lib().lnl_crc32c_batch_csr_dev(data.data_ptr(), offsets.data_ptr(), n, out.data_ptr(),
+                                             _stream_handle(stream)), "lnl_crc32c_batch_csr_dev")
+    return out
+
+
+def verify_csr(data, offsets, want_crc: bool = False, stream=None):
+    """Batched inbound layer: ok[i] = datagram i (trailing LE32 CRC included)
+    is >= 5 bytes and its CRC matches.  Returns ok (uint8) [, crc (int32)]."""
+    torch = _torch()
+    _check_dev_u8(data, "data")
+    _check_off(offsets, data)
+    n = offsets.numel() - 1
+    ok = torch.empty(max(n, 0), dtype=torch.uint8, device=data.device)
+    crc = torch.empty(max(n, 0), dtype=torch.int32, device=data.device) if want_crc else None
+    if n > 0:
+        check(lib().lnl_crc32c_verify_csr_dev(data.data_ptr(), offsets.data_ptr(), n, ok.data_ptr(),
+                                              crc.data_ptr() if crc is not None else None,
+                                              _stream_handle(stream)), "lnl_crc32c_verify_csr_dev")
+    return (ok, crc) if want_crc else ok
+
+
+def batch_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
+    """Host-resident batch over the GPU (H2D -> kernel -> D2H on 2 streams).
+    Blocking.  ``data`` uint8, ``offsets`` uint64/int64 with n+1 entries."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets).astype(np.uint64, copy=False)
+    n = offsets.size - 1
+    out = np.empty(max(n, 0), dtype=np.uint32)
+    if n > 0:
+        check(lib().lnl_crc32c_batch_host(data.ctypes.data, offsets.ctypes.data, n, out.ctypes.data,
+                                          device), "lnl_crc32c_batch_host")
+    return out

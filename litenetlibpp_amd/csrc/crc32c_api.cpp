@@ -1,0 +1,267 @@
+// crc32c_api.cpp -- the batched (GPU) side of the C ABI, include/lnl_crc32c.h.
+//
+// Thin: argument checks, per-device lazy state (a 16-byte dummy line the
+// kernels point idle LDS-DMA lanes at, the CU count for the persistent grid,
+// host-path staging buffers), and kernel launches on the caller's stream.
+// No batch entry point computes on the CPU: without a usable gfx950 device
+// every one of them fails with -ENODEV.
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <mutex>
+#include <string>
+
+#include "../../include/lnl_crc32c.h"
+#include "crc32c_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(-EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+constexpr int kMaxDevices = 64;
+
+struct DeviceState {
+    std::once_flag once;
+    int init_rc = 0;
+    std::string init_err;
+    uint8_t* dummy = nullptr;  // 256 zero bytes of device memory
+    int cus = 0;
+    bool gfx950 = false;
+    // host-path staging (guarded by host_mu)
+    std::mutex host_mu;
+    hipStream_t streams[2] = {nullptr, nullptr};
+    uint8_t* d_bytes[2] = {nullptr, nullptr};
+    uint64_t* d_off[2] = {nullptr, nullptr};
+    uint32_t* d_out[2] = {nullptr, nullptr};
+    size_t cap_bytes = 0, cap_n = 0;
+};
+
+DeviceState g_dev[kMaxDevices];
+
+int device_state(int dev, DeviceState** out) {
+    if (dev < 0 || dev >= kMaxDevices) return fail(-ENODEV, "device index %d out of range", dev);
+    DeviceState& S = g_dev[dev];
+    std::call_once(S.once, [&] {
+        hipDeviceProp_t prop;
+        hipError_t e = hipGetDeviceProperties(&prop, dev);
+        if (e != hipSuccess) {
+            S.init_rc = -ENODEV;
+            S.init_err = std::string("hipGetDeviceProperties: ") + hipGetErrorString(e);
+            return;
+        }
+        S.gfx950 = strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+        if (!S.gfx950) {
+            S.init_rc = -ENODEV;
+            S.init_err = std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950";
+            return;
+        }
+        S.cus = prop.multiProcessorCount;
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(dev);
+        e = hipMalloc(&S.dummy, 256);
+        if (e == hipSuccess) e = hipMemset(S.dummy, 0, 256);
+        (void)hipSetDevice(cur);
+        if (e != hipSuccess) {
+            S.init_rc = -ENOMEM;
+            S.init_err = std::string("device scratch allocation: ") + hipGetErrorString(e);
+        }
+    });
+    if (S.init_rc) return fail(S.init_rc, "%s", S.init_err.c_str());
+    *out = &S;
+    return 0;
+}
+
+int current_device(DeviceState** S) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fail(-ENODEV, "no HIP device: %s", hipGetErrorString(e));
+    return device_state(dev, S);
+}
+
+int grid_for(const DeviceState& S, uint32_t n) {
+    const uint32_t waves = (n + 63u) / 64u;
+    const uint32_t wgs = (waves + (lnl::kBlockThreads / 64) - 1) / (lnl::kBlockThreads / 64);
+    const uint32_t cap = (uint32_t)S.cus * (uint32_t)(lnl::kWavesPerCU / (lnl::kBlockThreads / 64));
+    return (int)std::max(1u, std::min(wgs, cap));
+}
+
+int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
+    a.dummy = S.dummy;
+    hipError_t e = lnl::launch_crc32c_batch(a, mode, grid_for(S, a.n), st);
+    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" const char* lnl_crc32c_last_error(void) { return g_err.c_str(); }
+
+extern "C" int lnl_crc32c_abi_version(void) { return LNL_CRC32C_ABI_VERSION; }
+
+extern "C" int lnl_crc32c_batch_fixed_dev(const uint8_t* d_base, size_t stride, uint32_t len,
+                                          uint32_t n, uint32_t* d_out, void* hip_stream) {
+    if (n == 0) return 0;
+    if (!d_out) return fail(-EINVAL, "d_out is NULL");
+    if (!d_base && len) return fail(-EINVAL, "d_base is NULL");
+    DeviceState* S;
+    if (int rc = current_device(&S)) return rc;
+    hipStream_t st = (hipStream_t)hip_stream;
+    if (len == 0) {  // CRC-32C of zero bytes is 0
+        hipError_t e = hipMemsetAsync(d_out, 0, (size_t)n * 4u, st);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
+    lnl::BatchArgs a{};
+    a.base = d_base;
+    a.stride = stride;
+    a.len = len;
+    a.n = n;
+    a.out = d_out;
+    return launch(*S, a, lnl::kModeFixed, st);
+}
+
+extern "C" int lnl_crc32c_batch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                        uint32_t* d_out, void* hip_stream) {
+    if (n == 0) return 0;
+    if (!d_out || !d_off) return fail(-EINVAL, "d_out / d_off is NULL");
+    if (!d_base) return fail(-EINVAL, "d_base is NULL");
+    DeviceState* S;
+    if (int rc = current_device(&S)) return rc;
+    lnl::BatchArgs a{};
+    a.base = d_base;
+    a.off = d_off;
+    a.n = n;
+    a.out = d_out;
+    return launch(*S, a, lnl::kModeCsr, (hipStream_t)hip_stream);
+}
+
+extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                         uint8_t* d_ok, uint32_t* d_crc, void* hip_stream) {
+    if (n == 0) return 0;
+    if (!d_ok || !d_off) return fail(-EINVAL, "d_ok / d_off is NULL");
+    if (!d_base) return fail(-EINVAL, "d_base is NULL");
+    DeviceState* S;
+    if (int rc = current_device(&S)) return rc;
+    lnl::BatchArgs a{};
+    a.base = d_base;
+    a.off = d_off;
+    a.n = n;
+    a.out = d_crc;
+    a.ok = d_ok;
+    return launch(*S, a, lnl::kModeVerify, (hipStream_t)hip_stream);
+}
+
+// Host-resident batch: chunks of whole datagrams alternate over two streams;
+// each chunk is H2D (bytes + offsets) -> kernel (offsets rebased by off0) ->
+// D2H (CRCs).  Stream order makes buffer reuse safe; the two streams overlap
+// one chunk's copies with the other's kernel.
+extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
+                                     uint32_t* h_out, int device) {
+    if (n == 0) return 0;
+    if (!h_base || !h_off || !h_out) return fail(-EINVAL, "NULL argument");
+    for (uint32_t i = 0; i < n; ++i)
+        if (h_off[i + 1] < h_off[i]) return fail(-EINVAL, "offsets decrease at %u", i);
+    DeviceState* S;
+    if (int rc = device_state(device, &S)) return rc;
+    std::lock_guard<std::mutex> lk(S->host_mu);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    struct Restore {
+        int d;
+        ~Restore() { (void)hipSetDevice(d); }
+    } restore{prev};
+
+    constexpr size_t kChunkBytes = size_t(64) << 20;  // per stream
+    constexpr uint32_t kChunkN = 1u << 16;
+    // chunk boundaries: <= kChunkN datagrams and <= kChunkBytes bytes (a single
+    // larger datagram gets a chunk of its own)
+    size_t need_bytes = 0;
+    uint32_t need_n = 0;
+    {
+        uint32_t i = 0;
+        while (i < n) {
+            uint32_t j = i + 1;
+            while (j < n && j - i < kChunkN && h_off[j + 1] - h_off[i] <= kChunkBytes) ++j;
+            need_bytes = std::max<size_t>(need_bytes, h_off[j] - h_off[i]);
+            need_n = std::max(need_n, j - i);
+            i = j;
+        }
+    }
+    if (!S->streams[0]) {
+        for (int k = 0; k < 2; ++k)
+            if ((e = hipStreamCreateWithFlags(&S->streams[k], hipStreamNonBlocking)) != hipSuccess)
+                return hip_fail(e, "hipStreamCreate");
+    }
+    if (need_bytes > S->cap_bytes || need_n > S->cap_n) {
+        for (int k = 0; k < 2; ++k) {
+            (void)hipFree(S->d_bytes[k]);
+            (void)hipFree(S->d_off[k]);
+            (void)hipFree(S->d_out[k]);
+            S->d_bytes[k] = nullptr;
+            S->d_off[k] = nullptr;
+            S->d_out[k] = nullptr;
+        }
+        S->cap_bytes = S->cap_n = 0;
+        const size_t nb = std::max<size_t>(need_bytes, 256);
+        for (int k = 0; k < 2; ++k) {
+            if ((e = hipMalloc(&S->d_bytes[k], nb)) != hipSuccess ||
+                (e = hipMalloc(&S->d_off[k], (size_t)(need_n + 1) * 8)) != hipSuccess ||
+                (e = hipMalloc(&S->d_out[k], (size_t)need_n * 4)) != hipSuccess)
+                return fail(-ENOMEM, "staging allocation: %s", hipGetErrorString(e));
+        }
+        S->cap_bytes = nb;
+        S->cap_n = need_n;
+    }
+    uint32_t i = 0;
+    int k = 0;
+    while (i < n) {
+        uint32_t j = i + 1;
+        while (j < n && j - i < kChunkN && h_off[j + 1] - h_off[i] <= kChunkBytes) ++j;
+        const uint32_t cn = j - i;
+        const size_t cb = h_off[j] - h_off[i];
+        hipStream_t st = S->streams[k];
+        if (cb && (e = hipMemcpyAsync(S->d_bytes[k], h_base + h_off[i], cb, hipMemcpyHostToDevice, st)) !=
+                      hipSuccess)
+            return hip_fail(e, "H2D bytes");
+        if ((e = hipMemcpyAsync(S->d_off[k], h_off + i, (size_t)(cn + 1) * 8, hipMemcpyHostToDevice, st)) !=
+            hipSuccess)
+            return hip_fail(e, "H2D offsets");
+        lnl::BatchArgs a{};
+        a.base = S->d_bytes[k];
+        a.off = S->d_off[k];
+        a.off0 = h_off[i];
+        a.n = cn;
+        a.out = S->d_out[k];
+        if (int rc = launch(*S, a, lnl::kModeCsr, st)) return rc;
+        if ((e = hipMemcpyAsync(h_out + i, S->d_out[k], (size_t)cn * 4, hipMemcpyDeviceToHost, st)) !=
+            hipSuccess)
+            return hip_fail(e, "D2H");
+        i = j;
+        k ^= 1;
+    }
+    for (int s = 0; s < 2; ++s)
+        if ((e = hipStreamSynchronize(S->streams[s])) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return 0;
+}

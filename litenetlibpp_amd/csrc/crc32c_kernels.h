@@ -1,0 +1,29 @@
+// crc32c_kernels.h -- launch interface between the C ABI (crc32c_api.cpp) and
+// the gfx950 kernels (crc32c_kernels.hip).  Internal; not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lnl {
+
+constexpr int kBlockThreads = 256;  // 4 waves; 64 KiB LDS -> 2 workgroups per CU
+constexpr int kWavesPerCU = 8;
+
+enum : int { kModeFixed = 0, kModeCsr = 1, kModeVerify = 2 };
+
+struct BatchArgs {
+    const uint8_t* base;   // d_base
+    const uint64_t* off;   // CSR offsets (n + 1), modes Csr / Verify
+    uint64_t off0;         // subtracted from every offset (host chunking: chunk-relative)
+    uint64_t stride;       // mode Fixed
+    uint32_t len;          // mode Fixed
+    uint32_t n;            // datagrams
+    uint32_t* out;         // CRC per datagram (may be null in Verify mode)
+    uint8_t* ok;           // Verify mode: 1 = trailing CRC matches
+    const uint8_t* dummy;  // 16 readable bytes (library scratch) for idle glds lanes
+};
+
+// Enqueue one batch kernel on `stream` with `grid` workgroups.
+hipError_t launch_crc32c_batch(const BatchArgs& a, int mode, int grid, hipStream_t stream);
+
+}  // namespace lnl

@@ -1,0 +1,99 @@
+"""The C-ABI boundary without a GPU: the library loads, exports every entry
+point include/lnl_crc32c.h declares, the per-datagram CPU half matches the
+oracle, and the batch half refuses to run (no CPU fallback) when no gfx950
+device is present."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lnl_crc32c.h")
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    import litenetlibpp_amd as P
+    if not os.path.exists(P.LIB_PATH):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "litenetlibpp_amd")], check=True,
+                       capture_output=True)
+    return P
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*[\w ]+?\**\s*\**(lnl_crc32c\w*)\s*\(", txt, re.M)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("lnl_crc32c", "lnl_crc32c_extend", "lnl_crc32c_batch_fixed_dev",
+              "lnl_crc32c_batch_csr_dev", "lnl_crc32c_batch_host", "lnl_crc32c_verify_csr_dev",
+              "lnl_crc32c_layer_outbound", "lnl_crc32c_layer_inbound", "lnl_crc32c_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    out = subprocess.run(["nm", "-D", "--defined-only", pkg.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (lnl_\w+)", out))
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    assert pkg.lib().lnl_crc32c_abi_version() == 1
+
+
+def test_cpu_crc_matches_oracle(pkg):
+    rng = np.random.default_rng(11)
+    assert pkg.crc32c(b"123456789") == 0xE3069283
+    assert pkg.crc32c(b"") == 0
+    for L in list(range(0, 200)) + [1399, 1400, 1432, 9000, 65507]:
+        d = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        assert pkg.crc32c(d) == oracle.crc(d, "bitwise"), L
+
+
+def test_cpu_extend(pkg):
+    rng = np.random.default_rng(12)
+    a = rng.integers(0, 256, 1001, dtype=np.uint8).tobytes()
+    b = rng.integers(0, 256, 433, dtype=np.uint8).tobytes()
+    assert pkg.crc32c_extend(pkg.crc32c(a), b) == pkg.crc32c(a + b)
+    assert pkg.crc32c_extend(0, a) == pkg.crc32c(a)
+    assert pkg.crc32c_extend(pkg.crc32c(a), b"") == pkg.crc32c(a)
+
+
+def test_layer_roundtrip_and_drop(pkg):
+    layer = pkg.Crc32cLayer()
+    payload = bytes([0x0B]) + bytes(range(200))   # header byte (MERGED) + body
+    shared = bytearray(b"xx" + payload + b"yy")    # send_raw's const shared buffer
+    before = bytes(shared)
+    wire = layer.process_outbound(shared, 2, len(payload))
+    assert bytes(shared) == before                 # source untouched
+    assert wire[:-4] == payload and len(wire) == len(payload) + 4
+    assert int.from_bytes(wire[-4:], "little") == oracle.crc(payload, "bitwise")
+    assert layer.process_inbound(wire) == payload
+    bad = bytearray(wire)
+    bad[7] ^= 0x40
+    assert layer.process_inbound(bytes(bad)) is None
+    assert layer.process_inbound(wire[:4]) is None   # < header + CRC
+    assert layer.process_inbound(pkg.Crc32cLayer().process_outbound(b"\x01")) == b"\x01"
+    assert layer.dropped == 2
+    assert pkg.mtu_with_layer(1432) == 1428
+
+
+def test_batch_entry_points_refuse_without_gpu(pkg):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present; covered by the gpu suite")
+    L = pkg.lib()
+    buf = (ctypes.c_uint8 * 64)()
+    out = (ctypes.c_uint32 * 4)()
+    rc = L.lnl_crc32c_batch_fixed_dev(ctypes.addressof(buf), 16, 16, 4, ctypes.addressof(out), None)
+    assert rc == -19, rc            # -ENODEV, never a CPU answer
+    assert L.lnl_crc32c_last_error()
+    assert list(out) == [0, 0, 0, 0]
+    # n == 0 is valid and touches nothing
+    assert L.lnl_crc32c_batch_fixed_dev(None, 0, 0, 0, None, None) == 0
