@@ -1,8 +1,9 @@
 // crc32c_api.cpp -- the batched (GPU) side of the C ABI, include/lnl_crc32c.h.
 //
 // Thin: argument checks, per-device lazy state (a 16-byte dummy line the
-// kernels point idle LDS-DMA lanes at, the CU count for the persistent grid,
-// host-path staging buffers), and kernel launches on the caller's stream.
+// kernels point idle LDS-DMA lanes at, the 12 KiB fold tables, the CU count
+// for the persistent grid, host-path staging buffers), and kernel launches on
+// the caller's stream.
 // No batch entry point computes on the CPU: without a usable gfx950 device
 // every one of them fails with -ENODEV.
 #include <errno.h>
@@ -17,6 +18,7 @@
 #include <string>
 
 #include "../../include/lnl_crc32c.h"
+#include "crc32c_bitslice.h"
 #include "crc32c_kernels.h"
 
 namespace {
@@ -45,6 +47,7 @@ struct DeviceState {
     int init_rc = 0;
     std::string init_err;
     uint8_t* dummy = nullptr;  // 256 zero bytes of device memory
+    uint32_t* fold = nullptr;  // fold tables (lnl_build_fold_tables), 12 KiB
     int cus = 0;
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)
@@ -79,8 +82,13 @@ int device_state(int dev, DeviceState** out) {
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(dev);
+        static uint32_t host_fold[LNL_FOLD_TABLE_WORDS];
+        static std::once_flag fold_once;
+        std::call_once(fold_once, [] { lnl_build_fold_tables(host_fold); });
         e = hipMalloc(&S.dummy, 256);
         if (e == hipSuccess) e = hipMemset(S.dummy, 0, 256);
+        if (e == hipSuccess) e = hipMalloc(&S.fold, sizeof host_fold);
+        if (e == hipSuccess) e = hipMemcpy(S.fold, host_fold, sizeof host_fold, hipMemcpyHostToDevice);
         (void)hipSetDevice(cur);
         if (e != hipSuccess) {
             S.init_rc = -ENOMEM;
@@ -108,6 +116,7 @@ int grid_for(const DeviceState& S, uint32_t n) {
 
 int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
     a.dummy = S.dummy;
+    a.fold = S.fold;
     hipError_t e = lnl::launch_crc32c_batch(a, mode, grid_for(S, a.n), st);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     return 0;

@@ -1,26 +1,33 @@
 // crc32c_bitslice.h -- the per-lane algebra of the batched CRC-32C kernels.
 //
-// One lane owns one datagram.  The datagram is cut into 128-byte ROWS that are
-// aligned to its END (the first row is front-padded with `pad` virtual zero
-// bytes, pad = 128*T - L, T = ceil(L/128)).  Word j (bytes 4j..4j+3) of every
-// row belongs to STREAM j, j = 0..31.  The 32 streams are processed together
-// BIT-SLICED: register S[i] holds bit i of the CRC register of all 32 streams,
-// stream j in bit j.  Per row:
+// One lane owns one datagram.  The datagram is read as 128-byte ROWS that are
+// the 128-byte-aligned memory lines it touches (line alignment is what the
+// HBM path wants: a row that straddles two lines costs a second line fetch).
+// Word j (bytes 4j..4j+3) of every row belongs to STREAM j, j = 0..31.  The
+// 32 streams are processed together BIT-SLICED: register S[i] holds bit i of
+// the CRC register of all 32 streams, stream j in bit j.  Per row:
 //
 //     X = transpose32(row words)            X[k] bit j = word j bit k
+//     X &= keep, X ^= inv                   (first / last rows only)
 //     S = M_128(S) ^ X                      (generated XOR network)
 //
 // where M_n is the CRC-32C "advance over n zero bytes" operator (linear over
-// GF(2); the networks are in crc32c_networks.inc).  After the last row, stream
-// s holds Q_s = sum_t M_128^(T-1-t) w_{s,t} and the raw CRC of the datagram is
+// GF(2); the networks are in crc32c_networks.inc).  The masks zero the `pad`
+// bytes of the first line that precede the datagram and the `e` bytes of the
+// last line that follow it, so the rows spell 0^pad || M || 0^e.  Leading
+// zeros do not change a raw (init 0) CRC; trailing ones multiply it by
+// M_e.  After the last row, with T rows, stream s holds
+// Q_s = sum_t M_128^(T-1-t) w_{s,t} and
 //
-//     R = M_4( sum_s M_{4(31-s)} Q_s )
+//     raw(M) = M_e^-1( M_4( sum_s M_{4(31-s)} Q_s ) ) = M_{4-e}( tree(Q) )
 //
-// computed by a 5-level bit-sliced tree (level l combines streams 2^l apart
-// with M_{4*2^(l-1)}), a 32-bit gather of bit 0 of every register and one
-// scalar M_4.  CRC-32C's init 0xFFFFFFFF is applied by XORing 0xFF into the
-// first 4 real bytes (valid for L >= 4; shorter datagrams use a constant), and
-// xorout by a final XOR, so no per-length table is needed.
+// tree(Q) is a 5-level bit-sliced fold (level l combines streams 2^l apart
+// with M_{4*2^(l-1)}) followed by a 32-bit gather of bit 0 of every register;
+// M_{4-e} is applied with two nibble tables (e = 16a + b:
+// M_{4-e} = M_{4-b} o M_{-16a}; 24 matrices, lnl_build_fold_tables).
+// CRC-32C's init 0xFFFFFFFF is applied by XORing 0xFF into the first 4 real
+// bytes (valid for L >= 4; shorter datagrams use a constant), and xorout by a
+// final XOR, so no per-length table is needed.
 //
 // This file is compiled twice: by hipcc into the gfx950 kernels (LNL_XOR3 is
 // then v_bitop3_b32 0x96) and by g++ into the host-side unit test that checks
@@ -107,19 +114,38 @@ LNL_HD LNL_INLINE void lnl_transpose32(uint32_t* a) {
 #undef LNL_TSTAGE
 }
 
-// Masks for the first real rows of a datagram.  In bit-sliced form byte b of
-// a row is stream b>>2, bit range 8*(b&3) .. +7, so the masks depend only on
-// q = k>>3.  keep[q] zeroes the `pad` virtual bytes of row 0; inv0[q]/inv1[q]
-// XOR the init 0xFFFFFFFF into the first four real bytes (only when len >= 4).
-// Those four bytes spill into row 1 when pad > 124 (len = 1..3 mod 128).
-LNL_HD LNL_INLINE void lnl_first_row_masks(uint32_t pad, uint32_t len, uint32_t* keep,
-                                           uint32_t* inv0, uint32_t* inv1) {
+// Masks for row `rel` of a datagram (rel = row index within the datagram,
+// negative for the virtual rows of a lane whose datagram spans fewer lines
+// than the wave's longest).  In bit-sliced form byte b of a row is stream
+// b>>2, bit range 8*(b&3) .. +7, so the masks depend only on q = k>>3.
+//   keep: zero the `pad` bytes before the datagram (rel == 0) and the `e`
+//         bytes after it (rel == T-1); everything on virtual rows.
+//   inv:  XOR the init 0xFFFFFFFF into the first four real bytes (len >= 4);
+//         they spill into row 1 when pad > 124.
+LNL_HD LNL_INLINE void lnl_row_masks(int32_t rel, uint32_t T, uint32_t pad, uint32_t e,
+                                     uint32_t len, uint32_t* keep, uint32_t* inv) {
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t e = (pad + 3u - q) >> 2;  // first stream whose byte 4e+q >= pad
-        keep[q] = e >= 32u ? 0u : (0xFFFFFFFFu << e);
-        inv0[q] = (e >= 32u || len < 4u) ? 0u : (1u << e);
-        inv1[q] = (e == 32u && len >= 4u) ? 1u : 0u;  // byte 128+q of the padded datagram
+        uint32_t k = 0xFFFFFFFFu, v = 0u;
+        if (rel < 0) {
+            k = 0u;
+        } else {
+            const uint32_t h = (pad + 3u - q) >> 2;  // first stream whose byte 4h+q >= pad
+            if (rel == 0) {
+                k = h >= 32u ? 0u : (0xFFFFFFFFu << h);
+                v = (h >= 32u || len < 4u) ? 0u : (1u << h);
+            } else if (rel == 1) {
+                v = (h == 32u && len >= 4u) ? 1u : 0u;  // byte 128+q of the padded datagram
+            }
+            if ((uint32_t)rel == T - 1u) {
+                // keep streams j with 4j + q <= 127 - e
+                const int32_t lim = 127 - (int32_t)e - (int32_t)q;
+                const uint32_t cnt = lim < 0 ? 0u : (uint32_t)(lim >> 2) + 1u;
+                k &= cnt >= 32u ? 0xFFFFFFFFu : ((1u << cnt) - 1u);
+            }
+        }
+        keep[q] = k;
+        inv[q] = v;
     }
 }
 
@@ -128,21 +154,47 @@ LNL_HD LNL_INLINE void lnl_apply_masks(uint32_t* x, const uint32_t* keep, const 
     for (int k = 0; k < 32; ++k) x[k] = (x[k] & keep[k >> 3]) ^ inv[k >> 3];
 }
 
-LNL_HD LNL_INLINE void lnl_apply_inv(uint32_t* x, const uint32_t* inv) {
-#pragma unroll
-    for (int k = 0; k < 32; ++k) x[k] ^= inv[k >> 3];
-}
 
-// One reflected CRC step per bit, 32 times: the scalar M_4 on one register.
-LNL_HD LNL_INLINE uint32_t lnl_adv4_scalar(uint32_t c) {
-#pragma unroll
-    for (int b = 0; b < 32; ++b) c = (c >> 1) ^ (LNL_CRC32C_POLY & (0u - (c & 1u)));
+// ---- fold tables: R = M_{4-e}(tree) for e = 16a + b ----------------------
+// 24 matrices stored as 8 nibble tables of 16 words each (128 words):
+// matrix m, table k, entry v = N_m(v << 4k).  m = 0..15: M_{4-b}; m = 16..23:
+// M_{-16a}.  Built on the host (lnl_build_fold_tables), staged into LDS by the
+// kernel, applied with 8 lookups per matrix.
+#define LNL_FOLD_TABLE_WORDS (24 * 128)
+
+// n reflected CRC steps forward (n > 0) or backward (n < 0) on one register.
+LNL_HD LNL_INLINE uint32_t lnl_step_bits(uint32_t c, int32_t n) {
+    for (; n > 0; --n) c = (c >> 1) ^ (LNL_CRC32C_POLY & (0u - (c & 1u)));
+    for (; n < 0; ++n) {  // POLY has bit 31 set: the top bit says whether it was xored
+        const uint32_t top = c >> 31;
+        c = ((c ^ (LNL_CRC32C_POLY & (0u - top))) << 1) | top;
+    }
     return c;
 }
 
-// Combine the 32 stream states into the raw CRC of the datagram (see header).
-// s is destroyed.
-LNL_HD LNL_INLINE uint32_t lnl_finalize(uint32_t* s) {
+LNL_HD LNL_INLINE void lnl_build_fold_tables(uint32_t* t) {
+    for (int m = 0; m < 24; ++m) {
+        const int32_t nbits = m < 16 ? 8 * (4 - m) : -128 * (m - 16);
+        for (int k = 0; k < 8; ++k)
+            for (uint32_t v = 0; v < 16; ++v) t[m * 128 + k * 16 + v] = lnl_step_bits(v << (4 * k), nbits);
+    }
+}
+
+// Table index of the two matrices for tail padding e (0..127).
+LNL_HD LNL_INLINE uint32_t lnl_fold_a(uint32_t e) { return 16u + (e >> 4); }
+LNL_HD LNL_INLINE uint32_t lnl_fold_b(uint32_t e) { return e & 15u; }
+
+// Host/emulation form of one matrix application (the kernel does the same 8
+// lookups from LDS in inline asm).
+LNL_HD LNL_INLINE uint32_t lnl_fold_apply(const uint32_t* mat, uint32_t v) {
+    uint32_t r = 0;
+    for (int k = 0; k < 8; ++k) r ^= mat[k * 16 + ((v >> (4 * k)) & 15u)];
+    return r;
+}
+
+// Combine the 32 stream states into tree(Q) = M_4^-1(raw CRC of the padded
+// rows) (see header).  s is destroyed.
+LNL_HD LNL_INLINE uint32_t lnl_fold_tree(uint32_t* s) {
     uint32_t t[32], z[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) t[k] = s[k] >> 1;
@@ -162,5 +214,5 @@ LNL_HD LNL_INLINE uint32_t lnl_finalize(uint32_t* s) {
     uint32_t r = 0;
 #pragma unroll
     for (int k = 31; k >= 0; --k) r = (r << 1) | (z[k] & 1u);
-    return lnl_adv4_scalar(r);
+    return r;
 }

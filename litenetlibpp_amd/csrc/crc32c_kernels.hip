@@ -1,31 +1,41 @@
 // crc32c_kernels.hip -- batched CRC-32C over UDP datagrams for gfx950 (MI355X).
 //
 // One wavefront owns a BATCH of 64 datagrams, one per lane.  Every datagram is
-// processed as end-aligned 128-byte rows (see crc32c_bitslice.h for the
-// algebra): the wave streams rows HBM -> LDS with global_load_lds_dwordx4
-// (LDS-DMA, no VGPR staging), each lane reads its own row back with
-// 8 x ds_read_b128, transposes it into 32 bit-sliced words and runs one
-// generated XOR network (S = M_128(S) ^ X) -- ~420 VALU ops per 128 bytes, no
-// tables, no bank conflicts, no MFMA (CRC is a GF(2) polynomial remainder, not
-// a dense contraction).  After the last row a 5-level bit-sliced tree folds the
-// 32 streams and each lane stores one uint32.
+// processed as the 128-byte-aligned memory lines it touches (see
+// crc32c_bitslice.h for the algebra): the wave streams lines HBM -> LDS with
+// global_load_lds_dwordx4 (LDS-DMA, no VGPR staging), each lane reads its own
+// row back with 8 x ds_read_b128, transposes it into 32 bit-sliced words and
+// runs one generated XOR network (S = M_128(S) ^ X) -- ~420 VALU ops per 128
+// bytes, no tables in the row loop, no bank conflicts, no MFMA (CRC is a GF(2)
+// polynomial remainder, not a dense contraction).  After the last row a
+// 5-level bit-sliced tree folds the 32 streams, two nibble-table lookups undo
+// the line padding, and each lane stores one uint32.
+//
+// Why lines: a row that straddles two 128-byte lines makes the LDS-DMA fetch
+// both lines (measured: 2^20 x 1408 B rows 128-B aligned 250 us, the same
+// shifted by 4..64 bytes 280 us; with nt loads 223 us vs 400 us).  Rows are
+// therefore the aligned lines themselves and each lane masks the bytes of its
+// first/last line that belong to neighbouring datagrams.  A 128-byte-aligned
+// line never crosses a page, so reading the whole first/last line of a
+// datagram is always safe even at the ends of the caller's buffer (those
+// bytes are read, never written, and masked).
 //
 // Memory pipeline per wave: two 8 KiB LDS row buffers; row s+2 is issued as
 // soon as row s has been read into registers, so two rows (16 KiB) per wave and
-// 128 KiB per CU (8 waves) are in flight while the wave computes.  HBM access:
-// each glds wave-instruction moves 8 datagrams x 128 contiguous bytes; the LDS
-// image is XOR-swizzled on the SOURCE address (slot = piece ^ ((row>>1)&7)) so
-// that the per-lane ds_read_b128 of a whole row is bank-conflict free.
+// 128 KiB per CU (8 waves) are in flight while the wave computes.  Each glds
+// wave-instruction moves 8 datagrams x 1 line; the LDS image is XOR-swizzled
+// on the SOURCE address (slot = piece ^ ((row>>1)&7)) so that the per-lane
+// ds_read_b128 of a whole row is bank-conflict free.
 //
-// The row reads are one inline-asm block (8 x ds_read_b128 + lgkmcnt(0)):
+// LDS reads are inline asm (8 x ds_read_b128 + lgkmcnt(0) in ONE statement):
 // hipcc would otherwise put `s_waitcnt vmcnt(0)` in front of any LDS read that
 // follows an LDS-DMA, draining the prefetched rows every step.  Row arrival is
-// instead waited for with a counted `s_waitcnt vmcnt(8)` (exactly 8 VMEM
-// instructions per row are ever issued, see issue_row).
+// waited for with a counted `s_waitcnt vmcnt(8)` (exactly 8 VMEM instructions
+// per row are ever issued, see issue_row).
 //
 // Waves are persistent (grid = min(batches, CUs x 8 waves)) and stride over
 // batches, so rows of the next batch are prefetched under the current batch's
-// last rows and its finalize.
+// last rows and its fold.
 //
 // Hot path of BASELINE configs 2-4 (fixed stride, CSR, sharded fixed stride)
 // and of the batched inbound verify; boundary: include/lnl_crc32c.h.
@@ -35,6 +45,15 @@
 #include "crc32c_bitslice.h"
 #include "crc32c_kernels.h"
 
+// Build knobs (defaults are the shipped configuration):
+//   LNL_GLDS_AUX   cache-policy bits of the LDS-DMA loads (0 = default, 2 = nt)
+//   LNL_DIAG_NO_COMPUTE  diagnostic build only: rows are loaded and read but the
+//                  transpose/network is replaced by an XOR (wrong CRCs) -- used
+//                  to measure the memory pipeline's own ceiling.
+#ifndef LNL_GLDS_AUX
+#define LNL_GLDS_AUX 2
+#endif
+
 namespace lnl {
 
 namespace {
@@ -43,6 +62,8 @@ constexpr int kWaves = kBlockThreads / 64;  // waves per workgroup
 constexpr int kRowU4 = 8;                   // one 128-byte row = 8 x uint4
 constexpr int kBufU4 = 64 * kRowU4;         // one row buffer = 64 rows = 8 KiB
 constexpr uint32_t kBufBytes = kBufU4 * 16;
+constexpr int kFoldU4 = LNL_FOLD_TABLE_WORDS / 4;  // 12 KiB of fold tables
+constexpr int kLdsU4 = kWaves * 2 * kBufU4 + kFoldU4;
 
 __device__ LNL_INLINE uint32_t swz(uint32_t row) { return (row >> 1) & 7u; }
 
@@ -54,19 +75,20 @@ __device__ LNL_INLINE uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfir
 // whose 16-byte piece this lane fetches.
 struct Batch {
     uint32_t valid;      // uniform: batch exists
-    uint32_t rows;       // uniform: max over lanes of ceil(len/128)
+    uint32_t rows;       // uniform: max over lanes of T
     uint32_t max_first;  // uniform: max over lanes of `first`
-    uint32_t simple;     // uniform: no idle lane and no near-base datagram
-    uint32_t any_nb;     // uniform: some datagram's first window starts before d_base
+    uint32_t simple;     // uniform: no idle lane
     // compute lane
     uint32_t p;      // datagram index (>= n: idle lane)
     uint32_t len;    // bytes covered by the CRC
-    uint32_t first;  // first real row of this lane (rows before it are virtual zeros)
-    uint32_t nb;     // this lane's first window starts before d_base: filled by hand
-    int64_t win;     // byte offset (from d_base) of the lane's first real window
-    // load lanes: absolute address of row 0 of datagram q (piece included)
+    uint32_t T;      // lines the datagram touches (0: idle)
+    uint32_t first;  // first real row of this lane (rows before it are virtual)
+    uint32_t pad;    // bytes of the first line before the datagram
+    uint32_t e;      // bytes of the last line after the datagram
+    // load lanes: absolute address of row 0 (line of datagram q minus first_q
+    // lines), piece included, and first_q | idle << 30
     uint64_t ladr[8];
-    uint32_t lfirst[8];  // first real row of q | 1<<30 idle | 1<<31 near-base
+    uint32_t lfirst[8];
 };
 
 template <int kMode>
@@ -110,23 +132,20 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
     uint32_t len;
     B.p = B.valid ? b * 64u + lane : a.n;
     lane_extent<kMode>(a, B.p, start, len);
-    const uint32_t T = (len + 127u) >> 7;
-    const uint32_t pad = (T << 7) - len;
+    const uint64_t abs0 = (uint64_t)(uintptr_t)a.base + start;
+    const uint64_t abs1 = abs0 + len - 1u;  // last byte (unused when len == 0)
+    const uint32_t idle = len == 0u ? 1u : 0u;
     B.len = len;
-    if constexpr (kMode == kModeFixed)
-        B.rows = uni(B.valid ? (a.len + 127u) >> 7 : 0u);  // idle lanes: last batch only
-    else
-        B.rows = uni(wave_max(T));
-    B.first = B.rows - T;
-    B.max_first = uni(wave_max(B.first));
-    B.win = (int64_t)start - (int64_t)pad;
-    const uint32_t idle = (T == 0u || B.p >= a.n) ? 1u : 0u;
-    B.nb = (!idle && (int64_t)start < (int64_t)pad) ? 1u : 0u;
-    B.any_nb = uni(__any(B.nb) ? 1u : 0u);
-    B.simple = uni(__any(idle | B.nb) ? 0u : 1u);
-    // row t of datagram q starts at d_base + win_q + 128 (t - first_q)
-    const uint64_t row0 = (uint64_t)(uintptr_t)a.base + (uint64_t)(B.win - ((int64_t)B.first << 7));
-    const uint32_t fl = B.first | (idle << 30) | (B.nb << 31);
+    B.T = idle ? 0u : (uint32_t)((abs1 >> 7) - (abs0 >> 7)) + 1u;
+    B.pad = (uint32_t)abs0 & 127u;
+    B.e = 127u - ((uint32_t)abs1 & 127u);
+    B.rows = uni(wave_max(B.T));
+    B.first = B.rows - B.T;
+    B.max_first = uni(wave_max(idle ? 0u : B.first));
+    B.simple = uni(__any(idle) ? 0u : 1u);
+    // row t of datagram q is line (abs0_q >> 7) + t - first_q
+    const uint64_t row0 = ((abs0 >> 7) << 7) - ((uint64_t)B.first << 7);
+    const uint32_t fl = B.first | (idle << 30);
     const uint32_t sub = lane >> 3, slot = lane & 7u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -139,47 +158,26 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
 }
 
 // Issue the 8 LDS-DMA instructions that bring row t of batch B into `buf`.
-// All 8 are issued unconditionally (inactive lanes fetch a 16-byte dummy line
-// into a slot that is masked): the counted `s_waitcnt vmcnt(8)` in the main
-// loop relies on exactly 8 VMEM instructions per row.
+// All 8 are issued unconditionally (lanes of idle datagrams or virtual rows
+// fetch a 16-byte dummy line into a slot that is masked): the counted
+// `s_waitcnt vmcnt(8)` in the main loop relies on exactly 8 VMEM
+// instructions per row.
 __device__ LNL_INLINE void issue_row(const BatchArgs& a, const Batch& B, uint32_t t, uint4* buf) {
     const uint64_t dt = (uint64_t)t << 7;
     if (B.simple && t > B.max_first) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(B.ladr[i] + dt),
-                                             (void*)(buf + 64 * i), 16, 0, 0);
+                                             (void*)(buf + 64 * i), 16, 0, LNL_GLDS_AUX);
     } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t f = B.lfirst[i];
-            const uint32_t first = f & 0x3FFFFFFFu;
-            bool on = !(f & (1u << 30)) && t >= first;
-            if (f & (1u << 31)) on = on && t != first;  // near-base first row: filled by hand
+            const bool on = !(f & (1u << 30)) && t >= (f & 0x3FFFFFFFu);
             const uint64_t src = on ? B.ladr[i] + dt : (uint64_t)(uintptr_t)a.dummy;
             __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (void*)(buf + 64 * i), 16,
-                                             0, 0);
+                                             0, LNL_GLDS_AUX);
         }
-    }
-}
-
-// Rare path: the lane's first window starts before d_base (a datagram within
-// 127 bytes of the buffer start).  The glds lanes fetched a dummy line for that
-// row; the lane writes its row image itself from in-bounds bytes only (the
-// bytes before d_base are virtual padding and get masked anyway).
-__device__ LNL_INLINE void fill_near_base_row(const BatchArgs& a, int64_t win, uint4* buf,
-                                              uint32_t lane) {
-    uint32_t* row = reinterpret_cast<uint32_t*>(buf + lane * kRowU4);
-#pragma unroll 1
-    for (int w = 0; w < 32; ++w) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int64_t off = win + 4 * w + b;
-            const uint32_t byte = off >= 0 ? a.base[off] : 0u;
-            v |= byte << (8 * b);
-        }
-        row[4 * (((uint32_t)w >> 2) ^ swz(lane)) + (w & 3)] = v;
     }
 }
 
@@ -213,6 +211,29 @@ __device__ LNL_INLINE void read_row(const uint32_t* ad, uint32_t* x) {
     }
 }
 
+// One fold matrix applied to v: 8 nibble lookups in the LDS copy of the fold
+// tables (inline asm for the same reason as read_row).
+__device__ LNL_INLINE uint32_t fold_apply_lds(uint32_t mat_base, uint32_t v) {
+    uint32_t ad[8], r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ad[k] = mat_base + 4u * (16u * k + ((v >> (4 * k)) & 15u));
+    asm volatile(
+        "ds_read_b32 %0, %8\n\t"
+        "ds_read_b32 %1, %9\n\t"
+        "ds_read_b32 %2, %10\n\t"
+        "ds_read_b32 %3, %11\n\t"
+        "ds_read_b32 %4, %12\n\t"
+        "ds_read_b32 %5, %13\n\t"
+        "ds_read_b32 %6, %14\n\t"
+        "ds_read_b32 %7, %15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
+          "=&v"(r[7])
+        : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7])
+        : "memory");
+    return LNL_XOR3(LNL_XOR3(r[0], r[1], r[2]), LNL_XOR3(r[3], r[4], r[5]), r[6] ^ r[7]);
+}
+
 template <int kMode>
 __device__ LNL_INLINE void store_result(const BatchArgs& a, const Batch& B, uint32_t crc) {
     if (B.p >= a.n) return;
@@ -235,10 +256,20 @@ __device__ LNL_INLINE void store_result(const BatchArgs& a, const Batch& B, uint
 
 template <int kMode>
 __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArgs a) {
-    __shared__ __attribute__((aligned(16))) uint4 lds[kWaves][2][kBufU4];
+    __shared__ __attribute__((aligned(16))) uint4 lds[kLdsU4];
     const uint32_t lane = __lane_id();
     const uint32_t wave = uni(threadIdx.x >> 6);
-    uint4* const buf_base = &lds[0][0][0] + wave * (2 * kBufU4);
+    uint4* const buf_base = lds + wave * (2 * kBufU4);
+    uint4* const fold_lds = lds + kWaves * 2 * kBufU4;
+    const uint32_t fold_base = (uint32_t)(uintptr_t)fold_lds;
+
+    // stage the fold tables (before any LDS-DMA is in flight)
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(a.fold);
+        for (int i = threadIdx.x; i < kFoldU4; i += kBlockThreads) fold_lds[i] = g[i];
+        __syncthreads();
+    }
+
     const uint32_t nbatch = (a.n + 63u) >> 6;
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint32_t nw = gridDim.x * kWaves;
@@ -301,10 +332,6 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (cur.any_nb && t <= cur.max_first) {
-            if (cur.nb && t == cur.first) fill_near_base_row(a, cur.win, buf, lane);
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        }
         uint32_t x[32];
         if (odd)
             read_row<kBufBytes>(rad, x);
@@ -325,27 +352,28 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
         have0 = have1;
         have1 = have2;
 
-        lnl_transpose32(x);
-        if (t <= cur.max_first + 1u) {
-            uint32_t keep[4], inv0[4], inv1[4];
-            lnl_first_row_masks((cur.rows - cur.first) * 128u - cur.len, cur.len, keep, inv0, inv1);
+#if defined(LNL_DIAG_NO_COMPUTE)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t kq = t < cur.first ? 0u : (t == cur.first ? keep[q] : 0xFFFFFFFFu);
-                const uint32_t iq = t == cur.first ? inv0[q] : (t == cur.first + 1u ? inv1[q] : 0u);
-                keep[q] = kq;
-                inv0[q] = iq;
-            }
-            lnl_apply_masks(x, keep, inv0);
+        for (int k = 0; k < 32; ++k) s[k] ^= x[k];
+#else
+        lnl_transpose32(x);
+        if (t <= cur.max_first + 1u || t + 1u == cur.rows) {
+            uint32_t keep[4], inv[4];
+            lnl_row_masks((int32_t)t - (int32_t)cur.first, cur.T, cur.pad, cur.e, cur.len, keep, inv);
+            lnl_apply_masks(x, keep, inv);
         }
         uint32_t o[32];
         lnl_net_adv128_x(s, x, o);
 #pragma unroll
         for (int k = 0; k < 32; ++k) s[k] = o[k];
+#endif
 
         ++step;
         if (++t == cur.rows) {
-            store_result<kMode>(a, cur, lnl_finalize(s) ^ lnl_final_xor(cur.len));
+            uint32_t r = lnl_fold_tree(s);
+            r = fold_apply_lds(fold_base + 512u * lnl_fold_a(cur.e), r);
+            r = fold_apply_lds(fold_base + 512u * lnl_fold_b(cur.e), r);
+            store_result<kMode>(a, cur, cur.T ? (r ^ lnl_final_xor(cur.len)) : 0u);
 #pragma unroll
             for (int k = 0; k < 32; ++k) s[k] = 0;
             t = 0;

@@ -1,10 +1,12 @@
 // Host-side check of the kernel's per-lane algebra (crc32c_bitslice.h) against
 // the oracle, without a GPU.  Each datagram is processed exactly as one lane
-// of the HIP kernel does: end-aligned 128-byte windows read from the shared
-// buffer (so the first window also contains bytes of the previous datagram,
-// which the masks must remove), transpose, M_128 network, finalize.
+// of the HIP kernel does: the 128-byte-aligned lines it touches are read from
+// the shared buffer (so the first and last rows also contain bytes of the
+// neighbouring datagrams, which the masks must remove), preceded by virtual
+// rows when the lane's wave needs more rows than the datagram has; transpose,
+// M_128 network, fold tree, M_{4-e} correction through the nibble tables.
 //
-// Build/run: driven by tests/test_emulation.py (g++ -O2).  Exit status 0 = all
+// Build/run: driven by tests/test_algebra.py (g++ -O2).  Exit status 0 = all
 // equal; mismatches are printed.
 #include <cstdint>
 #include <cstdio>
@@ -18,56 +20,69 @@
 extern "C" uint32_t oracle_crc32c_bitwise(const uint8_t* p, size_t n);
 extern "C" uint32_t oracle_crc32c_hw(const uint8_t* p, size_t n);
 
-static uint32_t lane_crc(const uint8_t* mem, size_t mem_len, size_t start, uint32_t len) {
-    const uint32_t T = (len + 127u) / 128u;
-    const uint32_t pad = 128u * T - len;
+static uint32_t g_fold[LNL_FOLD_TABLE_WORDS];
+
+// mem: the buffer; addresses are offsets into it and the buffer is treated as
+// starting on a 128-byte line.  `rows` >= the datagram's line count (extra
+// leading virtual rows, as in a wave whose longest datagram spans more lines).
+static uint32_t lane_crc(const uint8_t* mem, size_t mem_len, size_t start, uint32_t len,
+                         uint32_t extra_rows) {
+    if (len == 0) return 0;
+    const uint64_t line0 = start >> 7, line1 = (start + len - 1) >> 7;
+    const uint32_t T = (uint32_t)(line1 - line0 + 1);
+    const uint32_t pad = (uint32_t)(start & 127), e = 127u - (uint32_t)((start + len - 1) & 127);
+    const uint32_t rows = T + extra_rows, first = extra_rows;
     uint32_t s[32] = {0};
-    for (uint32_t t = 0; t < T; ++t) {
+    for (uint32_t t = 0; t < rows; ++t) {
+        const int32_t rel = (int32_t)t - (int32_t)first;
         uint32_t x[32];
-        // window bytes [start - pad + 128t, +128); bytes outside the buffer read 0xA5
         for (int w = 0; w < 32; ++w) {
             uint32_t v = 0;
             for (int b = 0; b < 4; ++b) {
-                long long a = (long long)start - pad + 128ll * t + 4 * w + b;
-                uint8_t byte = (a >= 0 && (size_t)a < mem_len) ? mem[a] : 0xA5;
+                // virtual rows read garbage (the kernel reads a dummy line there)
+                const long long a = rel < 0 ? -1 : (long long)((line0 + rel) << 7) + 4 * w + b;
+                const uint8_t byte = (a >= 0 && (size_t)a < mem_len) ? mem[a] : 0xA5;
                 v |= (uint32_t)byte << (8 * b);
             }
             x[w] = v;
         }
         lnl_transpose32(x);
-        uint32_t keep[4], inv0[4], inv1[4];
-        lnl_first_row_masks(pad, len, keep, inv0, inv1);
-        if (t == 0) lnl_apply_masks(x, keep, inv0);
-        if (t == 1) lnl_apply_inv(x, inv1);
+        uint32_t keep[4], inv[4];
+        lnl_row_masks(rel, T, pad, e, len, keep, inv);
+        lnl_apply_masks(x, keep, inv);
         uint32_t o[32];
         lnl_net_adv128_x(s, x, o);
         memcpy(s, o, sizeof s);
     }
-    return lnl_finalize(s) ^ lnl_final_xor(len);
+    uint32_t r = lnl_fold_tree(s);
+    r = lnl_fold_apply(g_fold + 128 * lnl_fold_a(e), r);
+    r = lnl_fold_apply(g_fold + 128 * lnl_fold_b(e), r);
+    return r ^ lnl_final_xor(len);
 }
 
 int main(int argc, char** argv) {
     const int max_len = argc > 1 ? atoi(argv[1]) : 1500;
+    lnl_build_fold_tables(g_fold);
     std::mt19937_64 rng(7);
     std::vector<uint8_t> mem(1 << 20);
     for (auto& b : mem) b = (uint8_t)rng();
     int bad = 0, checked = 0;
-    // every length 0..max_len at a few offsets, incl. offset 0 (window starts before the buffer)
     for (int len = 0; len <= max_len; ++len) {
-        for (size_t start : {size_t(0), size_t(1), size_t(4099), size_t(65536 + 3 * len)}) {
-            uint32_t got = lane_crc(mem.data(), mem.size(), start, (uint32_t)len);
-            uint32_t exp = oracle_crc32c_hw(mem.data() + start, len);
+        for (size_t start : {size_t(0), size_t(1), size_t(127), size_t(4099), size_t(65536 + 3 * len)}) {
+            const uint32_t extra = (uint32_t)(len % 3);
+            const uint32_t got = lane_crc(mem.data(), mem.size(), start, (uint32_t)len, extra);
+            const uint32_t exp = oracle_crc32c_hw(mem.data() + start, len);
             ++checked;
             if (got != exp) {
-                if (bad < 20) printf("MISMATCH len=%d start=%zu got=%08x exp=%08x\n", len, start, got, exp);
+                if (bad < 20)
+                    printf("MISMATCH len=%d start=%zu got=%08x exp=%08x\n", len, start, got, exp);
                 ++bad;
             }
         }
     }
-    // a few long ones, checked against the bitwise oracle
     for (uint32_t len : {4096u, 9000u, 65507u, 100003u}) {
-        uint32_t got = lane_crc(mem.data(), mem.size(), 12345, len);
-        uint32_t exp = oracle_crc32c_bitwise(mem.data() + 12345, len);
+        const uint32_t got = lane_crc(mem.data(), mem.size(), 12345, len, 1);
+        const uint32_t exp = oracle_crc32c_bitwise(mem.data() + 12345, len);
         ++checked;
         if (got != exp) {
             printf("MISMATCH len=%u got=%08x exp=%08x\n", len, got, exp);

@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Kernel-variant experiments (development tool, not the product path).
+
+build:  python tools/kvariants.py build           (here, hipcc cross-compiles)
+run:    python tools/kvariants.py run [--rounds R] (on the GPU box)
+
+Each variant is the product library compiled with extra -D flags.  All
+variants are timed in ONE process, interleaved over R rounds, on the same
+device-resident data (cdna_hip_programming.md section 5.4 rule 24), with HIP
+events on the launch stream; the median kernel time per variant is reported.
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VDIR = os.path.join(ROOT, "litenetlibpp_amd", "build", "variants")
+
+VARIANTS = {
+    "base": "",                                     # shipped: nt LDS-DMA loads
+    "dflt": "-DLNL_GLDS_AUX=0",                     # default cache policy
+    "nocomp": "-DLNL_DIAG_NO_COMPUTE",              # memory-pipeline ceiling (wrong CRCs)
+    "nocomp_dflt": "-DLNL_DIAG_NO_COMPUTE -DLNL_GLDS_AUX=0",
+}
+
+
+def build(names):
+    for n in names:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "litenetlibpp_amd"), "variant",
+                        f"NAME={n}", f"VFLAGS={VARIANTS[n]}"], check=True)
+        print("built", n)
+
+
+def run(names, rounds, workloads):
+    import numpy as np
+    import torch
+    libs = {}
+    for n in names:
+        L = ctypes.CDLL(os.path.join(VDIR, n + ".so"))
+        L.lnl_crc32c_batch_fixed_dev.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        libs[n] = L
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    results = {}
+    for (n_pk, L_pk, stride, shift) in workloads:
+        buf = torch.randint(0, 256, (n_pk * stride + 256,), dtype=torch.uint8, device=dev, generator=g)
+        data = buf[shift:]
+        out = torch.empty(n_pk, dtype=torch.int32, device=dev)
+        s = torch.cuda.current_stream()
+        times = {n: [] for n in names}
+        for r in range(rounds):
+            for n in names:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                libs[n].lnl_crc32c_batch_fixed_dev(data.data_ptr(), stride, L_pk, n_pk, out.data_ptr(), s.cuda_stream)
+                e0.record(s)
+                for _ in range(3):
+                    libs[n].lnl_crc32c_batch_fixed_dev(data.data_ptr(), stride, L_pk, n_pk, out.data_ptr(),
+                                                       s.cuda_stream)
+                e1.record(s)
+                torch.cuda.synchronize()
+                times[n].append(e0.elapsed_time(e1) / 3)
+        for n in names:
+            med = float(np.median(times[n]))
+            algo = n_pk * (L_pk + 4)
+            key = f"{n}@{n_pk}x{L_pk}/s{stride}+{shift}"
+            results[key] = {"us": round(med * 1e3, 2), "min_us": round(min(times[n]) * 1e3, 2),
+                            "GBps": round(algo / (med * 1e-3) / 1e9, 1)}
+            print(key, results[key], flush=True)
+    return results
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--names", default=",".join(VARIANTS))
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--workloads", default="1048576:1400:1400:0,1048576:1408:1408:0",
+                    help="n:len:stride:byte_shift,...")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kvariants.json"))
+    a = ap.parse_args()
+    names = a.names.split(",")
+    if a.cmd == "build":
+        build(names)
+    else:
+        wl = [tuple(int(v) for v in w.split(":")) for w in a.workloads.split(",")]
+        res = run(names, a.rounds, wl)
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
