@@ -47,7 +47,7 @@ struct DeviceState {
     int init_rc = 0;
     std::string init_err;
     uint8_t* dummy = nullptr;  // 256 zero bytes of device memory
-    uint32_t* fold = nullptr;  // fold tables (lnl_build_fold_tables), 12 KiB
+    uint32_t* fold = nullptr;  // kernel tables (lnl_build_tables), 12.5 KiB
     int cus = 0;
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)
@@ -82,9 +82,9 @@ int device_state(int dev, DeviceState** out) {
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(dev);
-        static uint32_t host_fold[LNL_FOLD_TABLE_WORDS];
+        static uint32_t host_fold[LNL_TABLE_WORDS];
         static std::once_flag fold_once;
-        std::call_once(fold_once, [] { lnl_build_fold_tables(host_fold); });
+        std::call_once(fold_once, [] { lnl_build_tables(host_fold); });
         e = hipMalloc(&S.dummy, 256);
         if (e == hipSuccess) e = hipMemset(S.dummy, 0, 256);
         if (e == hipSuccess) e = hipMalloc(&S.fold, sizeof host_fold);

@@ -21,7 +21,7 @@ struct BatchArgs {
     uint32_t* out;         // CRC per datagram (may be null in Verify mode)
     uint8_t* ok;           // Verify mode: 1 = trailing CRC matches
     const uint8_t* dummy;  // 16 readable bytes (library scratch) for idle glds lanes
-    const uint32_t* fold;  // LNL_FOLD_TABLE_WORDS words from lnl_build_fold_tables (device)
+    const uint32_t* fold;  // LNL_TABLE_WORDS words from lnl_build_tables (device)
 };
 
 // Enqueue one batch kernel on `stream` with `grid` workgroups.

@@ -4,21 +4,24 @@
 // processed as the 128-byte-aligned memory lines it touches (see
 // crc32c_bitslice.h for the algebra): the wave streams lines HBM -> LDS with
 // global_load_lds_dwordx4 (LDS-DMA, no VGPR staging), each lane reads its own
-// row back with 8 x ds_read_b128, transposes it into 32 bit-sliced words and
-// runs one generated XOR network (S = M_128(S) ^ X) -- ~420 VALU ops per 128
-// bytes, no tables in the row loop, no bank conflicts, no MFMA (CRC is a GF(2)
+// row back with 8 x ds_read_b128 -- 32 words that ARE the bit-sliced state
+// input (stream j = bit j of every word, no transpose) -- and runs one
+// generated XOR network (V = A V ^ X) -- ~165 VALU ops per 128 bytes, no
+// tables in the row loop, no bank conflicts, no MFMA (CRC is a GF(2)
 // polynomial remainder, not a dense contraction).  After the last row a
-// 5-level bit-sliced tree folds the 32 streams, two nibble-table lookups undo
-// the line padding, and each lane stores one uint32.
+// 5-level bit-sliced tree folds the 32 streams, two nibble-table lookups map
+// the result back to a CRC register and undo the line padding, and each lane
+// stores one uint32.
 //
 // Why lines: a row that straddles two 128-byte lines makes the LDS-DMA fetch
 // both lines (measured: 2^20 x 1408 B rows 128-B aligned 250 us, the same
 // shifted by 4..64 bytes 280 us; with nt loads 223 us vs 400 us).  Rows are
-// therefore the aligned lines themselves and each lane masks the bytes of its
-// first/last line that belong to neighbouring datagrams.  A 128-byte-aligned
-// line never crosses a page, so reading the whole first/last line of a
-// datagram is always safe even at the ends of the caller's buffer (those
-// bytes are read, never written, and masked).
+// therefore the aligned lines themselves; whole 16-byte pieces of a
+// datagram's first/last line that lie outside it are fetched from a zero line
+// instead, and each lane masks the one partial piece at either end.  A
+// 128-byte-aligned line never crosses a page, so reading the whole first/last
+// line of a datagram is always safe even at the ends of the caller's buffer
+// (those bytes are read, never written, and masked).
 //
 // Memory pipeline per wave: two 8 KiB LDS row buffers; row s+2 is issued as
 // soon as row s has been read into registers, so two rows (16 KiB) per wave and
@@ -48,7 +51,7 @@
 // Build knobs (defaults are the shipped configuration):
 //   LNL_GLDS_AUX   cache-policy bits of the LDS-DMA loads (0 = default, 2 = nt)
 //   LNL_DIAG_NO_COMPUTE  diagnostic build only: rows are loaded and read but the
-//                  transpose/network is replaced by an XOR (wrong CRCs) -- used
+//                  framing/network is replaced by an XOR (wrong CRCs) -- used
 //                  to measure the memory pipeline's own ceiling.
 #ifndef LNL_GLDS_AUX
 #define LNL_GLDS_AUX 2
@@ -62,7 +65,7 @@ constexpr int kWaves = kBlockThreads / 64;  // waves per workgroup
 constexpr int kRowU4 = 8;                   // one 128-byte row = 8 x uint4
 constexpr int kBufU4 = 64 * kRowU4;         // one row buffer = 64 rows = 8 KiB
 constexpr uint32_t kBufBytes = kBufU4 * 16;
-constexpr int kFoldU4 = LNL_FOLD_TABLE_WORDS / 4;  // 12 KiB of fold tables
+constexpr int kFoldU4 = LNL_TABLE_WORDS / 4;  // 12.5 KiB of tables (crc32c_bitslice.h)
 constexpr int kLdsU4 = kWaves * 2 * kBufU4 + kFoldU4;
 
 __device__ LNL_INLINE uint32_t swz(uint32_t row) { return (row >> 1) & 7u; }
@@ -85,8 +88,10 @@ struct Batch {
     uint32_t first;  // first real row of this lane (rows before it are virtual)
     uint32_t pad;    // bytes of the first line before the datagram
     uint32_t e;      // bytes of the last line after the datagram
+    uint32_t h;      // init vector for stream 31 (table H[pad])
     // load lanes: absolute address of row 0 (line of datagram q minus first_q
-    // lines), piece included, and first_q | idle << 30
+    // lines), piece included, and the framing of q:
+    // first_q | head piece hp_q << 20 | tail piece tp_q << 23 | idle << 30
     uint64_t ladr[8];
     uint32_t lfirst[8];
 };
@@ -122,8 +127,16 @@ __device__ LNL_INLINE uint32_t wave_max(uint32_t v) {
     return v;
 }
 
+// One LDS word read in inline asm (see read_row for why asm).
+__device__ LNL_INLINE uint32_t lds_read_u32(uint32_t addr) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+
 template <int kMode>
-__device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t nbatch, Batch& B) {
+__device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t nbatch, uint32_t tab_base,
+                                      Batch& B) {
     // Branch-free on purpose (every field written on every path keeps the
     // struct in registers).  An invalid batch (b >= nbatch) has only idle lanes.
     const uint32_t lane = __lane_id();
@@ -139,13 +152,14 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
     B.T = idle ? 0u : (uint32_t)((abs1 >> 7) - (abs0 >> 7)) + 1u;
     B.pad = (uint32_t)abs0 & 127u;
     B.e = 127u - ((uint32_t)abs1 & 127u);
+    B.h = lds_read_u32(tab_base + 4u * (LNL_TABLE_H_OFF + B.pad));
     B.rows = uni(wave_max(B.T));
     B.first = B.rows - B.T;
     B.max_first = uni(wave_max(idle ? 0u : B.first));
     B.simple = uni(__any(idle) ? 0u : 1u);
     // row t of datagram q is line (abs0_q >> 7) + t - first_q
     const uint64_t row0 = ((abs0 >> 7) << 7) - ((uint64_t)B.first << 7);
-    const uint32_t fl = B.first | (idle << 30);
+    const uint32_t fl = B.first | ((B.pad >> 4) << 20) | (((127u - B.e) >> 4) << 23) | (idle << 30);
     const uint32_t sub = lane >> 3, slot = lane & 7u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -158,22 +172,28 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
 }
 
 // Issue the 8 LDS-DMA instructions that bring row t of batch B into `buf`.
-// All 8 are issued unconditionally (lanes of idle datagrams or virtual rows
-// fetch a 16-byte dummy line into a slot that is masked): the counted
-// `s_waitcnt vmcnt(8)` in the main loop relies on exactly 8 VMEM
-// instructions per row.
+// All 8 are issued unconditionally -- lanes of idle datagrams, of virtual rows
+// and of whole pieces outside the datagram fetch the 16-byte zero line: the
+// counted `s_waitcnt vmcnt(8)` in the main loop relies on exactly 8 VMEM
+// instructions per row, and the algebra wants those bytes zero.
 __device__ LNL_INLINE void issue_row(const BatchArgs& a, const Batch& B, uint32_t t, uint4* buf) {
     const uint64_t dt = (uint64_t)t << 7;
-    if (B.simple && t > B.max_first) {
+    const uint32_t lane = __lane_id();
+    if (B.simple && t > B.max_first && t + 1u < B.rows) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(B.ladr[i] + dt),
                                              (void*)(buf + 64 * i), 16, 0, LNL_GLDS_AUX);
     } else {
+        const bool last = t + 1u == B.rows;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t f = B.lfirst[i];
-            const bool on = !(f & (1u << 30)) && t >= (f & 0x3FFFFFFFu);
+            const uint32_t first = f & 0xFFFFFu;
+            const uint32_t piece = (lane & 7u) ^ swz(8u * i + (lane >> 3));
+            const bool on = !(f & (1u << 30)) && t >= first &&
+                            !(t == first && piece < ((f >> 20) & 7u)) &&
+                            !(last && piece > ((f >> 23) & 7u));
             const uint64_t src = on ? B.ladr[i] + dt : (uint64_t)(uintptr_t)a.dummy;
             __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (void*)(buf + 64 * i), 16,
                                              0, LNL_GLDS_AUX);
@@ -263,7 +283,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
     uint4* const fold_lds = lds + kWaves * 2 * kBufU4;
     const uint32_t fold_base = (uint32_t)(uintptr_t)fold_lds;
 
-    // stage the fold tables (before any LDS-DMA is in flight)
+    // stage the tables (before any LDS-DMA is in flight)
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.fold);
         for (int i = threadIdx.x; i < kFoldU4; i += kBlockThreads) fold_lds[i] = g[i];
@@ -284,9 +304,9 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
 
     Batch cur, nxt;
     uint32_t b = gw;
-    make_batch<kMode>(a, b, nbatch, cur);
+    make_batch<kMode>(a, b, nbatch, fold_base, cur);
     if (!cur.valid) return;
-    make_batch<kMode>(a, b + nw, nbatch, nxt);
+    make_batch<kMode>(a, b + nw, nbatch, fold_base, nxt);
 
     // Row pipeline.  `step` counts computed rows; row `step` lives in buffer
     // step & 1.  have0: row `step` has been issued; have1: row step+1 has been
@@ -317,7 +337,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
             b += nw;
             cur = nxt;
             if (!cur.valid) break;
-            make_batch<kMode>(a, b + nw, nbatch, nxt);
+            make_batch<kMode>(a, b + nw, nbatch, fold_base, nxt);
             have0 = 0;  // nothing can have been issued for it
             have1 = 0;
             continue;
@@ -356,14 +376,16 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
 #pragma unroll
         for (int k = 0; k < 32; ++k) s[k] ^= x[k];
 #else
-        lnl_transpose32(x);
-        if (t <= cur.max_first + 1u || t + 1u == cur.rows) {
-            uint32_t keep[4], inv[4];
-            lnl_row_masks((int32_t)t - (int32_t)cur.first, cur.T, cur.pad, cur.e, cur.len, keep, inv);
-            lnl_apply_masks(x, keep, inv);
+        if (t <= cur.max_first || t + 1u == cur.rows) {
+            // framing: partial pieces at the datagram's ends, init injection
+            const bool head = t == cur.first && cur.T != 0u;
+            uint32_t hp, tp, hm[4], tm[4];
+            lnl_piece_masks(head, t + 1u == cur.rows, cur.pad, cur.e, hp, tp, hm, tm);
+            lnl_mask_row(x, hp, tp, hm, tm);
+            lnl_inject(s, cur.h, head);
         }
         uint32_t o[32];
-        lnl_net_adv128_x(s, x, o);
+        lnl_net_row_x(s, x, o);
 #pragma unroll
         for (int k = 0; k < 32; ++k) s[k] = o[k];
 #endif
@@ -371,16 +393,16 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
         ++step;
         if (++t == cur.rows) {
             uint32_t r = lnl_fold_tree(s);
-            r = fold_apply_lds(fold_base + 512u * lnl_fold_a(cur.e), r);
-            r = fold_apply_lds(fold_base + 512u * lnl_fold_b(cur.e), r);
-            store_result<kMode>(a, cur, cur.T ? (r ^ lnl_final_xor(cur.len)) : 0u);
+            r = fold_apply_lds(fold_base + 512u * lnl_table_b(cur.e), r);
+            r = fold_apply_lds(fold_base + 512u * lnl_table_a(cur.e), r);
+            store_result<kMode>(a, cur, cur.T ? ~r : 0u);
 #pragma unroll
             for (int k = 0; k < 32; ++k) s[k] = 0;
             t = 0;
             b += nw;
             cur = nxt;
             if (!cur.valid) break;
-            make_batch<kMode>(a, b + nw, nbatch, nxt);
+            make_batch<kMode>(a, b + nw, nbatch, fold_base, nxt);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

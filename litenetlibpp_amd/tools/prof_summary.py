@@ -35,8 +35,7 @@ def from_db(path):
     pmc = defaultdict(lambda: defaultdict(list))
     try:
         for name, counter, value in c.execute(
-                "select k.name, p.counter_name, p.value from pmc_events p join kernels k "
-                "on p.event_id = k.id"):
+                "select kernel_name, counter_name, value from counters_collection"):
             pmc[name][counter].append(value)
     except sqlite3.Error:
         pass
