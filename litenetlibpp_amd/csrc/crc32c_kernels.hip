@@ -50,11 +50,17 @@
 
 // Build knobs (defaults are the shipped configuration):
 //   LNL_GLDS_AUX   cache-policy bits of the LDS-DMA loads (0 = default, 2 = nt)
+//   LNL_EDGE_AUX   the same for the first/last rows of a batch
 //   LNL_DIAG_NO_COMPUTE  diagnostic build only: rows are loaded and read but the
 //                  framing/network is replaced by an XOR (wrong CRCs) -- used
 //                  to measure the memory pipeline's own ceiling.
 #ifndef LNL_GLDS_AUX
 #define LNL_GLDS_AUX 2
+#endif
+// cache policy of the first/last rows (the boundary line two neighbouring
+// datagrams share is fetched once by each)
+#ifndef LNL_EDGE_AUX
+#define LNL_EDGE_AUX 0
 #endif
 
 namespace lnl {
@@ -196,7 +202,7 @@ __device__ LNL_INLINE void issue_row(const BatchArgs& a, const Batch& B, uint32_
                             !(last && piece > ((f >> 23) & 7u));
             const uint64_t src = on ? B.ladr[i] + dt : (uint64_t)(uintptr_t)a.dummy;
             __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (void*)(buf + 64 * i), 16,
-                                             0, LNL_GLDS_AUX);
+                                             0, LNL_EDGE_AUX);
         }
     }
 }

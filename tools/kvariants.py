@@ -20,10 +20,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VDIR = os.path.join(ROOT, "litenetlibpp_amd", "build", "variants")
 
 VARIANTS = {
-    "base": "",                                     # shipped: nt LDS-DMA loads
+    "base": "",                                     # shipped: nt interior rows, default-policy edge rows
     "dflt": "-DLNL_GLDS_AUX=0",                     # default cache policy
     "nocomp": "-DLNL_DIAG_NO_COMPUTE",              # memory-pipeline ceiling (wrong CRCs)
     "nocomp_dflt": "-DLNL_DIAG_NO_COMPUTE -DLNL_GLDS_AUX=0",
+    "edge2": "-DLNL_EDGE_AUX=2",                    # nt on first/last rows too
+    "edge1": "-DLNL_EDGE_AUX=1",                    # sc0 on first/last rows
 }
 
 
