@@ -13,9 +13,9 @@ a MAX over per-rank times).  Inputs are generated on the device before the
 timed region.  Rank 0 prints ONE JSON line.
 
 roofline: algorithmic bytes per launch = sum(L) + 4 N (datagram bytes read +
-CRC words written; CSR adds 8 N offset bytes) over the average kernel time
-measured with HIP events on the launch stream; peak 8.0 TB/s (MI355X HBM3E
-nameplate).  traffic: HBM bytes per launch from the rocprofv3 PMC pass
+CRC words written; CSR adds 8 N offset bytes) over the average launch duration
+measured with one HIP event pair around the K launches on the launch stream;
+peak 8.0 TB/s (MI355X HBM3E nameplate).  traffic: HBM bytes per launch from the rocprofv3 PMC pass
 (profiles/traffic_<workload>.json, FETCH_SIZE x2 gfx950 correction +
 WRITE_SIZE) when present, else null.
 cpu_baseline: the oracle's batch CRC (SSE4.2 crc32 instruction, OpenMP) timed
@@ -37,6 +37,8 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from litenetlibpp_amd.shard import max_over_ranks, shard_range, sum_over_ranks  # noqa: E402
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E nameplate, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "CRC32C GB/s (device-resident) over 1M×1400B packets; bit-exact"
 
@@ -55,11 +57,12 @@ def parse():
     return ap.parse_args()
 
 
-def make_workload(args, rank, device):
-    """Device-resident synthetic batch (generated on the GPU, untimed)."""
+def make_workload(args, rank, world, device):
+    """Device-resident synthetic shard (generated on the GPU, untimed): rank r
+    owns datagrams shard_range(N * world, r, world) of the job's batch."""
     g = torch.Generator(device=device)
     g.manual_seed(42 + rank)
-    n = args.packets
+    _, n = shard_range(args.packets * world, rank, world)
     if args.workload == "fixed":
         L = args.length
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
@@ -145,51 +148,51 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs (the driver never sets them): LNL_BENCH_BACKEND=gloo and
+    # LNL_BENCH_ONE_GPU=1 run N ranks on one GPU to exercise the N > 1 path.
+    backend = os.environ.get("LNL_BENCH_BACKEND", "nccl")
+    gpu = 0 if os.environ.get("LNL_BENCH_ONE_GPU") == "1" else local
+    torch.cuda.set_device(gpu)
+    device = torch.device("cuda", gpu)
+    red_dev = device if backend == "nccl" else None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     import litenetlibpp_amd as P
     P.lib()
 
-    w = make_workload(args, rank, device)
+    w = make_workload(args, rank, world, device)
     out = torch.empty(w["n"], dtype=torch.int32, device=device)
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
         launch(P, w, out, stream)
     torch.cuda.synchronize()
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # K back-to-back launches bracketed by barrier + synchronize; one HIP event
+    # pair on the launch stream gives the average launch duration (per-launch
+    # event pairs would insert ~11 us of idle between launches)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
-        dist.barrier()
+        dist.barrier(device_ids=[gpu]) if backend == "nccl" else dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(stream)
+    e0.record(stream)
+    for _ in range(args.steps):
         launch(P, w, out, stream)
-        e1.record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
-        dist.barrier()
+        dist.barrier(device_ids=[gpu]) if backend == "nccl" else dist.barrier()
     wall = t1 - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if world > 1:
-        tt = torch.tensor([wall], dtype=torch.float64, device=device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall = float(tt.item())
-        kt = torch.tensor([kern_ms], dtype=torch.float64, device=device)
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-        kern_ms = float(kt.item())
-
+    kern_ms = e0.elapsed_time(e1) / args.steps
+    wall = max_over_ranks(wall, red_dev)          # the job takes as long as its slowest rank
+    kern_ms = max_over_ranks(kern_ms, red_dev)
     ms_per_step = wall / args.steps * 1e3
-    total_payload = w["payload"] * world  # identical shard sizes (fixed); csr: rank-0 estimate
-    if w["off"] is not None and world > 1:
-        tp = torch.tensor([w["payload"]], dtype=torch.float64, device=device)
-        dist.all_reduce(tp)
-        total_payload = float(tp.item())
+    total_payload = sum_over_ranks(w["payload"], red_dev)
     value = total_payload / (ms_per_step * 1e-3) / 1e9
     achieved = w["algo"] / (kern_ms * 1e-3) / 1e9
 

@@ -23,14 +23,15 @@
 // Framing.  Rows spell 0^pad || M || 0^e: the pad bytes of the first line
 // before the datagram and the e bytes of the last line after it are zero
 // (whole 16-byte pieces come from a zero line, the one partial piece at each
-// end is masked: lnl_piece_masks / lnl_mask_row).  Leading zeros leave a raw
+// end is masked: lnl_piece_masks; the kernel applies the masks to the piece
+// in LDS before the lane reads its row).  Leading zeros leave a raw
 // CRC unchanged; trailing ones multiply it by step^(8e), undone in the final
-// map.  CRC-32C's init 0xFFFFFFFF is INJECTED into the state at the
-// datagram's first row: a register value c at the start of that row equals
-// step^(8 pad)(c) at the datagram start, and a register value enters the
-// stream basis as stream 31, so the lane XORs bit k of
-// h = L^-1(step^(-8 pad)(0xFFFFFFFF)) into bit 31 of register k
-// (lnl_inject).  Then
+// map.  CRC-32C's init 0xFFFFFFFF enters at the datagram's first row: a
+// register value c at the start of that row equals step^(8 pad)(c) at the
+// datagram start, and a register value at the start of a message is the same
+// as XORing it into the message's first 32 bits -- here word 0 of the row, so
+// the lane XORs c0 = step^(-8 pad)(0xFFFFFFFF) into x[0] (table C[pad]).
+// Then
 //
 //     CRC(M) = step^(-8e)( L( fold(V) ) ) ^ 0xFFFFFFFF      (len >= 1; 0 for len 0)
 //
@@ -69,10 +70,10 @@
 // entry v = N(v << 4k), so N(x) = XOR_k table_k[nibble_k(x)].
 //   [  0 .. 16)  TB[b] = step^(-8b) o L        (b = e & 15)
 //   [ 16 .. 24)  TA[a] = step^(-128a)          (a = e >> 4)
-//   then 128 words H[pad] = L^-1(step^(-8 pad)(0xFFFFFFFF))
+//   then 128 words C[pad] = step^(-8 pad)(0xFFFFFFFF)
 #define LNL_TABLE_MATS 24
-#define LNL_TABLE_H_OFF (LNL_TABLE_MATS * 128)
-#define LNL_TABLE_WORDS (LNL_TABLE_H_OFF + 128)
+#define LNL_TABLE_C_OFF (LNL_TABLE_MATS * 128)
+#define LNL_TABLE_WORDS (LNL_TABLE_C_OFF + 128)
 
 // n reflected CRC steps forward (n > 0) or backward (n < 0) on one register.
 LNL_HD LNL_INLINE uint32_t lnl_step_bits(uint32_t c, int32_t n) {
@@ -94,36 +95,8 @@ LNL_HD LNL_INLINE uint32_t lnl_cols_apply(const uint32_t* cols, uint32_t v) {
 
 // Host-side table construction (also used by the CPU emulation test).
 LNL_HD inline void lnl_build_tables(uint32_t* t) {
-    uint32_t L[32], Li[32];
+    uint32_t L[32];
     for (int k = 0; k < 32; ++k) L[k] = lnl_step_bits(LNL_CRC32C_POLY, 992 - 32 * k);
-    // Gauss-Jordan inverse over GF(2): rows of [L | I]
-    uint32_t ra[32], rb[32];
-    for (int i = 0; i < 32; ++i) {
-        uint32_t r = 0;
-        for (int k = 0; k < 32; ++k) r |= ((L[k] >> i) & 1u) << k;
-        ra[i] = r;
-        rb[i] = 1u << i;
-    }
-    for (int c = 0; c < 32; ++c) {
-        int piv = c;
-        while (!((ra[piv] >> c) & 1u)) ++piv;
-        uint32_t tmp = ra[c];
-        ra[c] = ra[piv];
-        ra[piv] = tmp;
-        tmp = rb[c];
-        rb[c] = rb[piv];
-        rb[piv] = tmp;
-        for (int i = 0; i < 32; ++i)
-            if (i != c && ((ra[i] >> c) & 1u)) {
-                ra[i] ^= ra[c];
-                rb[i] ^= rb[c];
-            }
-    }
-    for (int k = 0; k < 32; ++k) {
-        uint32_t col = 0;
-        for (int i = 0; i < 32; ++i) col |= ((rb[i] >> k) & 1u) << i;
-        Li[k] = col;
-    }
     for (int m = 0; m < LNL_TABLE_MATS; ++m)
         for (int k = 0; k < 8; ++k)
             for (uint32_t v = 0; v < 16; ++v) {
@@ -131,8 +104,7 @@ LNL_HD inline void lnl_build_tables(uint32_t* t) {
                 t[m * 128 + k * 16 + v] =
                     m < 16 ? lnl_step_bits(lnl_cols_apply(L, x), -8 * m) : lnl_step_bits(x, -128 * (m - 16));
             }
-    for (int pad = 0; pad < 128; ++pad)
-        t[LNL_TABLE_H_OFF + pad] = lnl_cols_apply(Li, lnl_step_bits(0xFFFFFFFFu, -8 * pad));
+    for (int pad = 0; pad < 128; ++pad) t[LNL_TABLE_C_OFF + pad] = lnl_step_bits(0xFFFFFFFFu, -8 * pad);
 }
 
 LNL_HD LNL_INLINE uint32_t lnl_table_b(uint32_t e) { return e & 15u; }
@@ -182,14 +154,6 @@ LNL_HD LNL_INLINE void lnl_mask_row(uint32_t* x, uint32_t hp, uint32_t tp, const
         const uint32_t b = piece == tp ? tm[k & 3] : 0xFFFFFFFFu;
         x[k] &= a & b;
     }
-}
-
-// XOR the init-carrying vector h into stream 31 (bit 31 of every register)
-// when `on`.
-LNL_HD LNL_INLINE void lnl_inject(uint32_t* s, uint32_t h, bool on) {
-    const uint32_t m = on ? 0x80000000u : 0u;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) s[k] ^= (h << (31 - k)) & m;
 }
 
 // ---- fold ---------------------------------------------------------------

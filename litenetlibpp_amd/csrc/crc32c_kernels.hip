@@ -94,7 +94,7 @@ struct Batch {
     uint32_t first;  // first real row of this lane (rows before it are virtual)
     uint32_t pad;    // bytes of the first line before the datagram
     uint32_t e;      // bytes of the last line after the datagram
-    uint32_t h;      // init vector for stream 31 (table H[pad])
+    uint32_t c0;     // CRC init as the first row's word 0 (table C[pad])
     // load lanes: absolute address of row 0 (line of datagram q minus first_q
     // lines), piece included, and the framing of q:
     // first_q | head piece hp_q << 20 | tail piece tp_q << 23 | idle << 30
@@ -158,7 +158,7 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
     B.T = idle ? 0u : (uint32_t)((abs1 >> 7) - (abs0 >> 7)) + 1u;
     B.pad = (uint32_t)abs0 & 127u;
     B.e = 127u - ((uint32_t)abs1 & 127u);
-    B.h = lds_read_u32(tab_base + 4u * (LNL_TABLE_H_OFF + B.pad));
+    B.c0 = lds_read_u32(tab_base + 4u * (LNL_TABLE_C_OFF + B.pad));
     B.rows = uni(wave_max(B.T));
     B.first = B.rows - B.T;
     B.max_first = uni(wave_max(idle ? 0u : B.first));
@@ -235,6 +235,23 @@ __device__ LNL_INLINE void read_row(const uint32_t* ad, uint32_t* x) {
         x[4 * k + 2] = v[k].z;
         x[4 * k + 3] = v[k].w;
     }
+}
+
+// AND-mask one 16-byte piece of the lane's row in LDS (read, mask, write back;
+// the row read that follows sees the masked bytes: LDS ops of a wave execute
+// in order).  Asm for the same reason as read_row.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <uint32_t OFF>
+__device__ LNL_INLINE void patch_piece(uint32_t addr, const uint32_t* m) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr), "i"(OFF)
+                 : "memory");
+    v.x &= m[0];
+    v.y &= m[1];
+    v.z &= m[2];
+    v.w &= m[3];
+    asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
 }
 
 // One fold matrix applied to v: 8 nibble lookups in the LDS copy of the fold
@@ -358,11 +375,48 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // framing of the datagrams' first/last rows: the partial 16-byte piece
+        // at either end is masked in LDS (whole pieces outside the datagram
+        // were fetched from the zero line)
+        const bool edge = t <= cur.max_first || t + 1u == cur.rows;
+        const bool head = edge && t == cur.first && cur.T != 0u;
+#if !defined(LNL_MASK_IN_REGS)
+        if (edge) {
+            uint32_t hp, tp, hm[4], tm[4];
+            lnl_piece_masks(head, t + 1u == cur.rows, cur.pad, cur.e, hp, tp, hm, tm);
+            const uint32_t sw = swz(lane);
+            // lanes with no partial piece on this row patch piece 0 with all-ones
+            const uint32_t rowb = rad[0] - 16u * sw;  // piece 0 sits at slot sw
+            const uint32_t hsel = hp < 8u ? hp : 0u, tsel = tp < 8u ? tp : 0u;
+            uint32_t hmk[4], tmk[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                hmk[w] = hp < 8u ? hm[w] : 0xFFFFFFFFu;
+                tmk[w] = tp < 8u ? tm[w] : 0xFFFFFFFFu;
+            }
+            const uint32_t haddr = rowb + 16u * (hsel ^ sw), taddr = rowb + 16u * (tsel ^ sw);
+            if (odd) {
+                patch_piece<kBufBytes>(haddr, hmk);
+                patch_piece<kBufBytes>(taddr, tmk);
+            } else {
+                patch_piece<0>(haddr, hmk);
+                patch_piece<0>(taddr, tmk);
+            }
+        }
+#endif
         uint32_t x[32];
         if (odd)
             read_row<kBufBytes>(rad, x);
         else
             read_row<0>(rad, x);
+#if defined(LNL_MASK_IN_REGS)
+        if (edge) {
+            uint32_t hp, tp, hm[4], tm[4];
+            lnl_piece_masks(head, t + 1u == cur.rows, cur.pad, cur.e, hp, tp, hm, tm);
+            lnl_mask_row(x, hp, tp, hm, tm);
+        }
+#endif
+        if (edge) x[0] ^= head ? cur.c0 : 0u;  // CRC init, as the first row's word 0
         // prefetch row step+2 into the buffer just drained
         uint32_t have2 = 0;
         {
@@ -382,14 +436,6 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
 #pragma unroll
         for (int k = 0; k < 32; ++k) s[k] ^= x[k];
 #else
-        if (t <= cur.max_first || t + 1u == cur.rows) {
-            // framing: partial pieces at the datagram's ends, init injection
-            const bool head = t == cur.first && cur.T != 0u;
-            uint32_t hp, tp, hm[4], tm[4];
-            lnl_piece_masks(head, t + 1u == cur.rows, cur.pad, cur.e, hp, tp, hm, tm);
-            lnl_mask_row(x, hp, tp, hm, tm);
-            lnl_inject(s, cur.h, head);
-        }
         uint32_t o[32];
         lnl_net_row_x(s, x, o);
 #pragma unroll

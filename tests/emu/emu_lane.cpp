@@ -4,7 +4,7 @@
 // the shared buffer (so the first and last rows also contain bytes of the
 // neighbouring datagrams, which the zero line and the masks must remove),
 // preceded by virtual rows when the lane's wave needs more rows than the
-// datagram has; init injection, row network, fold tree, final tables.
+// datagram has; init XOR, row network, fold tree, final tables.
 //
 // Build/run: driven by tests/test_algebra.py (g++ -O2).  Exit status 0 = all
 // equal; mismatches are printed.
@@ -32,7 +32,7 @@ static uint32_t lane_crc(const uint8_t* mem, size_t mem_len, size_t start, uint3
     const uint32_t T = (uint32_t)(line1 - line0 + 1);
     const uint32_t pad = (uint32_t)(start & 127), e = 127u - (uint32_t)((start + len - 1) & 127);
     const uint32_t rows = T + extra_rows, first = extra_rows;
-    const uint32_t h = g_tab[LNL_TABLE_H_OFF + pad];
+    const uint32_t c0 = g_tab[LNL_TABLE_C_OFF + pad];
     uint32_t s[32] = {0};
     for (uint32_t t = 0; t < rows; ++t) {
         const int32_t rel = (int32_t)t - (int32_t)first;
@@ -54,7 +54,7 @@ static uint32_t lane_crc(const uint8_t* mem, size_t mem_len, size_t start, uint3
             x[w] = v;
         }
         if (head || tail) lnl_mask_row(x, hp, tp, hm, tm);
-        lnl_inject(s, h, head);
+        if (head) x[0] ^= c0;  // CRC init as the row's first word
         uint32_t o[32];
         lnl_net_row_x(s, x, o);
         memcpy(s, o, sizeof s);

@@ -26,6 +26,7 @@ VARIANTS = {
     "nocomp_dflt": "-DLNL_DIAG_NO_COMPUTE -DLNL_GLDS_AUX=0",
     "edge2": "-DLNL_EDGE_AUX=2",                    # nt on first/last rows too
     "edge1": "-DLNL_EDGE_AUX=1",                    # sc0 on first/last rows
+    "regmask": "-DLNL_MASK_IN_REGS",                # framing masks in registers, not LDS
 }
 
 
