@@ -35,6 +35,10 @@
  *   - Empty batches (n == 0) are valid and launch nothing.
  *   - No batch entry point ever computes on the CPU: without a usable GPU
  *     they fail with -ENODEV.
+ *   - Device kernels fetch whole 128-byte-aligned memory lines: they may READ
+ *     (never write) bytes of the same 128-byte line before the first / after
+ *     the last datagram.  Such a line never crosses a page, so this cannot
+ *     fault; the bytes are masked out of every CRC.
  */
 #ifndef LNL_CRC32C_H
 #define LNL_CRC32C_H

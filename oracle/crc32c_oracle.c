@@ -21,6 +21,10 @@
  * over exactly the bytes net_packet::data()[0 .. size()) (header byte included,
  * /root/reference/include/lnl/net_packet.h:112-118).
  *
+ * PARITY UNPINNED AGAINST THE REFERENCE: with no CRC in the reference there
+ * is no reference output, test or golden vector for this path, and no
+ * oracle/_ref build (nothing in /root/reference computes a checksum; upstream
+ * C# LiteNetLib's CRC32C.cs is not available offline).
  * Parity is therefore defined by the CRC-32C standard (Castagnoli):
  *   polynomial 0x1EDC6F41, reflected 0x82F63B78, refin = refout = true,
  *   init 0xFFFFFFFF, xorout 0xFFFFFFFF, check("123456789") = 0xE3069283,
