@@ -122,6 +122,41 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
     return 0;
 }
 
+// Lane-run plan for a fixed-stride batch (crc32c_run.hip): how many leading
+// datagrams the run kernel covers.  0 = use the batch kernel for all.
+#ifndef LNL_RUN_K
+#define LNL_RUN_K 8
+#endif
+uint32_t run_plan(size_t stride, uint32_t len, uint32_t n, lnl::RunArgs& r) {
+#if defined(LNL_NO_RUN)  // experiment builds only (tools/kvariants.py): batch kernel for everything
+    return 0;
+#endif
+    if (len < 129u || stride < len || stride > (1u << 20)) return 0;
+    const uint32_t S = (uint32_t)stride;
+    const uint32_t low = S & (0u - S);  // largest power of two dividing S
+    const uint32_t p = low >= 128u ? 1u : 128u / low;
+    const uint32_t k = LNL_RUN_K;
+    const uint32_t q = p > k ? p : k;
+    if ((uint64_t)64u * q * S >= (1ull << 31)) return 0;  // per-lane 32-bit offsets
+    const uint32_t super = 64u * q;
+    const uint32_t n_main = n - n % super;
+    if (n_main == 0) return 0;
+    r.stride = S;
+    r.len = len;
+    r.k = k;
+    r.q = q;
+    r.slices = q / k;
+    r.nb = n_main / (64u * k);
+    return n_main;
+}
+
+int grid_for_waves(const DeviceState& S, uint32_t waves) {
+    const uint32_t per_wg = lnl::kBlockThreads / 64;
+    const uint32_t wgs = (waves + per_wg - 1) / per_wg;
+    const uint32_t cap = (uint32_t)S.cus * (uint32_t)(lnl::kWavesPerCU / per_wg);
+    return (int)std::max(1u, std::min(wgs, cap));
+}
+
 }  // namespace
 
 extern "C" const char* lnl_crc32c_last_error(void) { return g_err.c_str(); }
@@ -140,12 +175,22 @@ extern "C" int lnl_crc32c_batch_fixed_dev(const uint8_t* d_base, size_t stride, 
         hipError_t e = hipMemsetAsync(d_out, 0, (size_t)n * 4u, st);
         return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
     }
+    lnl::RunArgs r{};
+    const uint32_t n_main = run_plan(stride, len, n, r);
+    if (n_main) {
+        r.base = d_base;
+        r.out = d_out;
+        r.fold = S->fold;
+        hipError_t e = lnl::launch_crc32c_run(r, grid_for_waves(*S, r.nb), st);
+        if (e != hipSuccess) return hip_fail(e, "kernel launch");
+        if (n_main == n) return 0;
+    }
     lnl::BatchArgs a{};
-    a.base = d_base;
+    a.base = d_base + (size_t)n_main * stride;
     a.stride = stride;
     a.len = len;
-    a.n = n;
-    a.out = d_out;
+    a.n = n - n_main;
+    a.out = d_out + n_main;
     return launch(*S, a, lnl::kModeFixed, st);
 }
 

@@ -15,7 +15,7 @@
 //
 //     V <- A V ^ X,   A = L^-1 step^1024 L        (X = the row's 32 words)
 //
-// (generated XOR network lnl_net_row_x, ~165 VALU ops per 128 bytes).  After
+// (generated XOR network lnl_net_row_x, ~150 VALU ops per 128 bytes).  After
 // the last row the register is L( sum_j B^(31-j) V_j ) with B = L^-1 step L:
 // a 5-level bit-sliced fold (level l combines streams 2^l apart with
 // B^(2^(l-1))) and a 32-bit gather of bit 0 of every register (lnl_fold_tree).
@@ -156,28 +156,60 @@ LNL_HD LNL_INLINE void lnl_mask_row(uint32_t* x, uint32_t hp, uint32_t tp, const
     }
 }
 
+// Word w of a row (bytes 4w .. 4w+3): keep the bytes at row offsets <= be /
+// >= bs.  (The lane-run kernel's datagram end / start masks; be, bs are
+// wave-uniform there, so these fold to scalar code.)
+// (Written as a clamped 64-bit shift: a handful of scalar ops per word.)
+LNL_HD LNL_INLINE uint32_t lnl_low_bits(int32_t n) {  // n clamped to [0, 32] low bits set
+    const int32_t c = n < 0 ? 0 : (n > 32 ? 32 : n);
+    return (uint32_t)((1ull << c) - 1ull);
+}
+LNL_HD LNL_INLINE uint32_t lnl_word_keep_le(int32_t w, uint32_t be) {
+    return lnl_low_bits(8 * (int32_t)be + 8 - 32 * w);
+}
+LNL_HD LNL_INLINE uint32_t lnl_word_keep_ge(int32_t w, uint32_t bs) {
+    return ~lnl_low_bits(8 * (int32_t)bs - 32 * w);
+}
+
 // ---- fold ---------------------------------------------------------------
 // sum_j B^(31-j) V_j gathered into one word (bit k = coordinate k).  s is
 // destroyed.
 LNL_HD LNL_INLINE uint32_t lnl_fold_tree(uint32_t* s) {
-    uint32_t t[32], z[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) t[k] = s[k] >> 1;
-    lnl_net_fold1_x(s, t, z);  // bit 2i: B V_2i ^ V_2i+1
-#pragma unroll
-    for (int k = 0; k < 32; ++k) t[k] = z[k] >> 2;
-    lnl_net_fold2_x(z, t, s);  // bit 4i
-#pragma unroll
-    for (int k = 0; k < 32; ++k) t[k] = s[k] >> 4;
-    lnl_net_fold4_x(s, t, z);  // bit 8i
-#pragma unroll
-    for (int k = 0; k < 32; ++k) t[k] = z[k] >> 8;
-    lnl_net_fold8_x(z, t, s);  // bit 16i
-#pragma unroll
-    for (int k = 0; k < 32; ++k) t[k] = s[k] >> 16;
-    lnl_net_fold16_x(s, t, z);  // bit 0: sum_j B^(31-j) V_j
+    uint32_t z[32];
+    lnl_net_fold1(s, z);  // bit 2i: B V_2i ^ V_2i+1
+    lnl_net_fold2(z, s);  // bit 4i
+    lnl_net_fold4(s, z);  // bit 8i
+    lnl_net_fold8(z, s);  // bit 16i
+    lnl_net_fold16(s, z);  // bit 0: sum_j B^(31-j) V_j
     uint32_t r = 0;
 #pragma unroll
     for (int k = 31; k >= 0; --k) r = (r << 1) | (z[k] & 1u);
     return r;
+}
+
+// The fold split for PAIRS of datagrams (lane-run kernel): level 1 per
+// datagram, then the two level-1 results -- meaningful at even bits only --
+// are interleaved (a at bits 2i, b at bits 2i+1) and levels 2..5 run once for
+// both: every level is the same shift-and-network on all bit positions, so a's
+// streams end at bit 0 and b's at bit 1.  ra / rb equal lnl_fold_tree of each.
+LNL_HD LNL_INLINE void lnl_fold_level1(const uint32_t* s, uint32_t* f) {
+    lnl_net_fold1(s, f);
+}
+
+LNL_HD LNL_INLINE void lnl_fold_pair(const uint32_t* a, const uint32_t* b, uint32_t& ra, uint32_t& rb) {
+    uint32_t s[32], z[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) s[k] = (a[k] & 0x55555555u) | ((b[k] << 1) & 0xAAAAAAAAu);
+    lnl_net_fold2(s, z);
+    lnl_net_fold4(z, s);
+    lnl_net_fold8(s, z);
+    lnl_net_fold16(z, s);
+    uint32_t x = 0, y = 0;
+#pragma unroll
+    for (int k = 31; k >= 0; --k) {
+        x = (x << 1) | (s[k] & 1u);
+        y = (y << 1) | ((s[k] >> 1) & 1u);
+    }
+    ra = x;
+    rb = y;
 }

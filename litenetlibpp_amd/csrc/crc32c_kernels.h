@@ -27,4 +27,21 @@ struct BatchArgs {
 // Enqueue one batch kernel on `stream` with `grid` workgroups.
 hipError_t launch_crc32c_batch(const BatchArgs& a, int mode, int grid, hipStream_t stream);
 
+// Fixed-stride lane-run kernel (crc32c_run.hip).  Covers datagrams
+// [0, nb * 64 * k) of the batch: wave-batch wb = g * slices + j, lane l owns
+// datagrams g*64q + l*q + j*k + [0, k).
+struct RunArgs {
+    const uint8_t* base;
+    uint64_t stride;       // S >= len
+    uint32_t len;          // >= 129
+    uint32_t k;            // datagrams per lane run (even)
+    uint32_t q;            // lane spacing in datagrams: q * S % 128 == 0, q % k == 0
+    uint32_t slices;       // q / k
+    uint32_t nb;           // wave-batches
+    uint32_t* out;
+    const uint32_t* fold;  // LNL_TABLE_WORDS words from lnl_build_tables (device)
+};
+
+hipError_t launch_crc32c_run(const RunArgs& a, int grid, hipStream_t stream);
+
 }  // namespace lnl

@@ -32,12 +32,13 @@ OUT = os.path.join(HERE, "..", "csrc", "crc32c_networks.inc")
 # (function name, message bits the operator advances, with_x)
 NETWORKS = [
     ("lnl_net_row_x", 1024, True),   # Horner row step: V <- A V ^ X (X = the row's words)
-    # fold tree, level l: V <- B^(2^(l-1)) V ^ (V >> 2^(l-1)) (x = the shift)
-    ("lnl_net_fold1_x", 1, True),
-    ("lnl_net_fold2_x", 2, True),
-    ("lnl_net_fold4_x", 4, True),
-    ("lnl_net_fold8_x", 8, True),
-    ("lnl_net_fold16_x", 16, True),
+    # fold tree, level l: V <- B^d V ^ (V >> d), d = 2^(l-1): the x term of
+    # output i is s[i] >> d, computed at its use (no 32-register shift array)
+    ("lnl_net_fold1", 1, "shr"),
+    ("lnl_net_fold2", 2, "shr"),
+    ("lnl_net_fold4", 4, "shr"),
+    ("lnl_net_fold8", 8, "shr"),
+    ("lnl_net_fold16", 16, "shr"),
 ]
 
 
@@ -57,23 +58,92 @@ def verify(net, nbits, with_x, trials=64):
                 raise AssertionError(f"network {nbits} wrong at bit {j}")
 
 
+def _peak_live(order, net, n_in=64):
+    """Peak number of simultaneously live values (inputs until their last use,
+    temporaries, produced outputs) when the ops run in `order`."""
+    last = {}
+    outs = set(o for o in net.outputs if o is not None)
+    for i, (_, srcs) in enumerate(order):
+        for x in srcs:
+            last[x] = i
+    live = set(k for k in range(n_in) if k in last)
+    peak = len(live)
+    for i, (d, srcs) in enumerate(order):
+        for x in srcs:
+            if last[x] == i and x not in outs:
+                live.discard(x)
+        live.add(d)
+        peak = max(peak, len(live))
+    return peak
+
+
+def _schedule(net, rng, n_in=64):
+    """List-schedule the ops to keep few values live: among the ready ops take
+    the one that frees the most operands (random tie-break)."""
+    ops = list(net.ops)
+    users = {}
+    for i, (_, srcs) in enumerate(ops):
+        for x in srcs:
+            users.setdefault(x, []).append(i)
+    outs = set(o for o in net.outputs if o is not None)
+    remaining = {x: len(u) for x, u in users.items()}
+    avail = set(range(n_in))
+    done = [False] * len(ops)
+    ready = {i for i, (_, srcs) in enumerate(ops) if all(x in avail for x in srcs)}
+    order = []
+    while ready:
+        best, bs = None, None
+        for i in sorted(ready):
+            _, srcs = ops[i]
+            freed = sum(1 for x in set(srcs) if remaining[x] == srcs.count(x) and x not in outs)
+            score = freed + rng.random() * 0.5
+            if bs is None or score > bs:
+                best, bs = i, score
+        ready.discard(best)
+        done[best] = True
+        d, srcs = ops[best]
+        order.append(ops[best])
+        for x in srcs:
+            remaining[x] -= 1
+        avail.add(d)
+        for j in users.get(d, []):
+            if not done[j] and all(x in avail for x in ops[j][1]):
+                ready.add(j)
+    assert len(order) == len(ops)
+    return order
+
+
+def low_pressure_order(net, tries=40):
+    best = list(net.ops)
+    bp = _peak_live(best, net)
+    for r in range(tries):
+        o = _schedule(net, random.Random(r))
+        p = _peak_live(o, net)
+        if p < bp:
+            best, bp = o, p
+    return best, bp
+
+
 def emit(name, nbits, with_x, net):
     lines = []
+    shr = with_x == "shr"
     sig = "const uint32_t* __restrict__ s, const uint32_t* __restrict__ x, uint32_t* __restrict__ o" \
-        if with_x else "const uint32_t* __restrict__ s, uint32_t* __restrict__ o"
-    what = f"o = (L^-1 step^{nbits} L)(s)" + (" ^ x" if with_x else "")
+        if with_x is True else "const uint32_t* __restrict__ s, uint32_t* __restrict__ o"
+    what = f"o = (L^-1 step^{nbits} L)(s)" + (f" ^ (s >> {nbits})" if shr else " ^ x" if with_x else "")
+    order, peak = low_pressure_order(net)
     lines.append(f"// {what}   [{net.cost()} ops, "
-                 f"{sum(1 for _, src in net.ops if len(src) == 3)} of them 3-input]")
+                 f"{sum(1 for _, src in net.ops if len(src) == 3)} of them 3-input; "
+                 f"ordered for <= {peak} live values]")
     lines.append(f"LNL_HD LNL_INLINE void {name}({sig}) {{")
 
     def ref(sig_id):
         if sig_id < 32:
             return f"s[{sig_id}]"
         if sig_id < 64:
-            return f"x[{sig_id - 32}]"
+            return f"(s[{sig_id - 32}] >> {nbits})" if shr else f"x[{sig_id - 32}]"
         return f"t{sig_id - (1 << 20)}"
 
-    for d, srcs in net.ops:
+    for d, srcs in order:
         if len(srcs) == 3:
             lines.append(f"  const uint32_t {ref(d)} = LNL_XOR3({ref(srcs[0])}, {ref(srcs[1])}, {ref(srcs[2])});")
         else:
@@ -96,8 +166,8 @@ def generate(restarts: int) -> str:
     for name, nbits, with_x in NETWORKS:
         rows = rows_of(stream_basis_matrix(nbits))
         extra = [32 + i for i in range(32)] if with_x else None
-        net = synthesize(rows, 32, extra_terms=extra, restarts=restarts)
-        verify(net, nbits, with_x)
+        net = synthesize(rows, 32, extra_terms=extra, restarts=restarts, greedy3_restarts=60)
+        verify(net, nbits, bool(with_x))
         parts.append(emit(name, nbits, with_x, net))
         parts.append("")
     return "\n".join(parts)

@@ -61,8 +61,48 @@ def _paar(rows: list[set], n_inputs: int, rng: random.Random | None):
     return rows, defs, nxt
 
 
+def _greedy3(rows: list[set], rng: random.Random, pair_weight: float):
+    """Greedy CSE that extracts 3-input common subexpressions as well as pairs.
+
+    A triple shared by c rows costs one XOR3 and saves about c ops downstream
+    (each row's XOR3 chain gets one term-pair shorter); a pair shared by c rows
+    saves about c/2.  Pick the best by that estimate (pair_weight tunes the
+    pair estimate; ties broken at random)."""
+    from itertools import combinations
+    rows = [set(r) for r in rows]
+    defs = {}
+    nxt = DERIVED_BASE
+    while True:
+        c3 = Counter()
+        c2 = Counter()
+        for r in rows:
+            rl = sorted(r)
+            c2.update(combinations(rl, 2))
+            if len(rl) >= 3:
+                c3.update(combinations(rl, 3))
+        b3 = max(c3.values()) if c3 else 0
+        b2 = max(c2.values()) if c2 else 0
+        g3 = b3 - 1 if b3 >= 2 else -1
+        g2 = (b2 * pair_weight - 1) if b2 >= 2 else -1
+        if g3 < 0 and g2 < 0:
+            break
+        if g3 >= g2:
+            t = rng.choice([k for k, v in c3.items() if v == b3])
+        else:
+            t = rng.choice([k for k, v in c2.items() if v == b2])
+        st = set(t)
+        sig = nxt
+        nxt += 1
+        defs[sig] = tuple(t)
+        for r in rows:
+            if st <= r:
+                r -= st
+                r.add(sig)
+    return rows, defs, nxt
+
+
 def synthesize(rows_bits: list[int], n_inputs: int, extra_terms: list | None = None,
-               restarts: int = 40, seed: int = 1) -> Net:
+               restarts: int = 40, seed: int = 1, greedy3_restarts: int = 0) -> Net:
     """rows_bits[i]: bitmask over inputs 0..n_inputs-1 for output i.
     extra_terms[i]: optional extra input id (>= n_inputs) xored into output i
     (each used once, e.g. the data word in a Horner step)."""
@@ -78,6 +118,13 @@ def synthesize(rows_bits: list[int], n_inputs: int, extra_terms: list | None = N
         net = _pack(rows, defs, n_inputs, extra_terms, DERIVED_BASE, n_total_inputs)
         if best is None or net.cost() < best.cost():
             best = net
+    for attempt in range(greedy3_restarts):
+        rng = random.Random(seed * 7919 + attempt)
+        pw = (0.5, 0.6, 0.75)[attempt % 3]
+        rows, defs, nxt = _greedy3(base_rows, rng, pw)
+        net = _pack(rows, defs, n_inputs, extra_terms, DERIVED_BASE, n_total_inputs)
+        if net.cost() < best.cost():
+            best = net
     return best
 
 
@@ -85,7 +132,7 @@ def _pack(rows, defs, n_inputs, extra_terms, first_new, n_total_inputs):
     """Turn Paar output into an XOR2/XOR3 op list with fusion of single-use
     intermediates."""
     # expression tree: each derived signal = multiset of operands
-    expr = {s: [a, b] for s, (a, b) in defs.items()}
+    expr = {s: list(v) for s, v in defs.items()}
     out_terms = []
     for i, r in enumerate(rows):
         t = sorted(r)

@@ -65,6 +65,96 @@ static uint32_t lane_crc(const uint8_t* mem, size_t mem_len, size_t start, uint3
     return r ^ 0xFFFFFFFFu;
 }
 
+// One lane of the lane-run kernel (crc32c_run.hip): K datagrams of len bytes
+// at stride S starting at mem offset A (len >= 129, S >= len, K even),
+// processed as the 128-byte lines from A's line on, with the kernel's
+// wave-uniform start / end events and the pairwise fold.
+static int run_lane(const uint8_t* mem, size_t A, uint32_t S, uint32_t len, uint32_t K,
+                    uint32_t* crc_out) {
+    const uint32_t ph = (uint32_t)(A & 127);
+    const size_t line0 = A - ph;
+    const uint32_t R = (ph + (K - 1) * S + len + 127) >> 7;
+    uint32_t s[32] = {0}, P[32] = {0};
+    uint32_t ks = 0, ke = 0, sb = ph, eb = ph + len - 1, eprev = 0;
+    for (uint32_t t = 0; t < R; ++t) {
+        uint32_t x[32];
+        memcpy(x, mem + line0 + 128 * (size_t)t, 128);
+        const bool st = ks < K && (sb >> 7) == t;
+        const bool en = ke < K && (eb >> 7) == t;
+        uint32_t o[32];
+        if (!st && !en) {
+            lnl_net_row_x(s, x, o);
+            memcpy(s, o, sizeof s);
+            continue;
+        }
+        uint32_t xe[32];
+        const uint32_t be = eb & 127u, bs = sb & 127u;
+        if (en) {
+            for (int w = 0; w < 32; ++w) xe[w] = x[w] & lnl_word_keep_le(w, be);
+            lnl_net_row_x(s, xe, o);
+        }
+        if (st) {
+            if (en && S == len)
+                for (int w = 0; w < 32; ++w) s[w] = x[w] ^ xe[w];
+            else
+                for (int w = 0; w < 32; ++w) s[w] = x[w] & lnl_word_keep_ge(w, bs);
+            s[0] ^= g_tab[LNL_TABLE_C_OFF + bs];
+            ++ks;
+            sb += S;
+        }
+        if (en) {
+            uint32_t f[32];
+            lnl_fold_level1(o, f);
+            if ((ke & 1u) == 0) {
+                memcpy(P, f, sizeof P);
+                eprev = 127u - be;
+            } else {
+                uint32_t ra, rb;
+                lnl_fold_pair(P, f, ra, rb);
+                const uint32_t eb2 = 127u - be;
+                ra = lnl_table_apply(g_tab + 128 * lnl_table_a(eprev), lnl_table_apply(g_tab + 128 * lnl_table_b(eprev), ra));
+                rb = lnl_table_apply(g_tab + 128 * lnl_table_a(eb2), lnl_table_apply(g_tab + 128 * lnl_table_b(eb2), rb));
+                crc_out[ke - 1] = ~ra;
+                crc_out[ke] = ~rb;
+            }
+            ++ke;
+            eb += S;
+        }
+    }
+    return (int)ke;
+}
+
+static int check_runs(const std::vector<uint8_t>& mem, int& checked) {
+    int bad = 0;
+    const uint32_t lens[] = {129, 130, 200, 255, 256, 257, 511, 1000, 1399, 1400, 1401, 1432, 4000};
+    const uint32_t gaps[] = {0, 1, 7, 100, 127, 128, 300};
+    for (uint32_t len : lens)
+        for (uint32_t gap : gaps)
+            for (uint32_t K : {2u, 4u, 8u})
+                for (uint32_t ph = 0; ph < 128; ph += 9) {
+                    const uint32_t S = len + gap;
+                    const size_t A = 4096 + ph;
+                    uint32_t got[8];
+                    const int nk = run_lane(mem.data(), A, S, len, K, got);
+                    if (nk != (int)K) {
+                        printf("RUN count len=%u S=%u K=%u ph=%u got %d\n", len, S, K, ph, nk);
+                        ++bad;
+                        continue;
+                    }
+                    for (uint32_t k = 0; k < K; ++k) {
+                        const uint32_t exp = oracle_crc32c_hw(mem.data() + A + (size_t)k * S, len);
+                        ++checked;
+                        if (got[k] != exp) {
+                            if (bad < 20)
+                                printf("RUN MISMATCH len=%u S=%u K=%u ph=%u k=%u got=%08x exp=%08x\n", len, S,
+                                       K, ph, k, got[k], exp);
+                            ++bad;
+                        }
+                    }
+                }
+    return bad;
+}
+
 int main(int argc, char** argv) {
     const int max_len = argc > 1 ? atoi(argv[1]) : 1500;
     lnl_build_tables(g_tab);
@@ -94,6 +184,7 @@ int main(int argc, char** argv) {
             ++bad;
         }
     }
+    bad += check_runs(mem, checked);
     printf("checked=%d bad=%d\n", checked, bad);
     return bad ? 1 : 0;
 }

@@ -70,6 +70,44 @@ def test_fixed_lengths(P, length):
         assert np.array_equal(got, exp), (length, stride, n)
 
 
+# (stride, len): the lane-run plan (crc32c_run.hip) covers whole superblocks of
+# 64 * max(8, 128 / gcd(stride, 128)) datagrams; the rest goes to the batch
+# kernel.  Odd strides (superblock 8192), strides that are multiples of 128,
+# gaps between datagrams (including gaps of whole rows), len = 129.
+RUN_CASES = [(1400, 1400), (1401, 1401), (1432, 1432), (1408, 1408), (130, 129), (129, 129),
+             (200, 129), (1500, 1400), (1600, 1400), (4096, 4000), (2048, 1400), (1404, 1400)]
+
+
+@pytest.mark.parametrize("stride,length", RUN_CASES)
+def test_fixed_lane_runs(P, stride, length):
+    low = stride & -stride
+    q = max(8, 1 if low >= 128 else 128 // low)
+    sb = 64 * q
+    rng = np.random.default_rng(stride * 7 + length)
+    for m, extra, shift in ((1, 0, 0), (2, 5, 3), (3, sb - 1, 127), (1, 100, 64)):
+        n = m * sb + extra
+        data = rng.integers(0, 256, shift + (n - 1) * stride + length, dtype=np.uint8)
+        d = dev(data)[shift:]
+        exp = oracle.batch_fixed(data[shift:], stride, length, n)
+        got = u32(P.batch_fixed(d, stride, length, n))
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (stride, length, n, shift, bad.size, bad[:5])
+
+
+def test_fixed_lane_runs_persistent_waves(P):
+    """More wave-batches than resident waves: waves loop over batches and
+    prefetch the next batch's rows under the current one's last rows."""
+    n = 3 * (1 << 19) + 777
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    d = torch.randint(0, 256, (n * 1400 + 1,), dtype=torch.uint8, device="cuda", generator=g)[1:]
+    got = u32(P.batch_fixed(d, 1400, 1400, n))
+    data = d.cpu().numpy()
+    exp = oracle.batch_fixed(data, 1400, 1400, n)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, (bad.size, bad[:5])
+
+
 def test_fixed_zero_length_and_empty_batch(P):
     data = torch.zeros(64, dtype=torch.uint8, device="cuda")
     out = torch.full((10,), -1, dtype=torch.int32, device="cuda")

@@ -20,7 +20,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VDIR = os.path.join(ROOT, "litenetlibpp_amd", "build", "variants")
 
 VARIANTS = {
-    "base": "",                                     # shipped: nt interior rows, default-policy edge rows
+    "base": "",                                     # shipped: lane-run kernel for fixed strides
+    "batch": "-DLNL_NO_RUN",                        # any-layout batch kernel for everything
+    "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
+    "k16": "-DLNL_RUN_K=16",
+    "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
     "dflt": "-DLNL_GLDS_AUX=0",                     # default cache policy
     "nocomp": "-DLNL_DIAG_NO_COMPUTE",              # memory-pipeline ceiling (wrong CRCs)
     "nocomp_dflt": "-DLNL_DIAG_NO_COMPUTE -DLNL_GLDS_AUX=0",
