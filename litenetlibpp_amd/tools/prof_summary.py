@@ -16,6 +16,8 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    if "crc32c_run_kernel" in name:
+        return "crc32c_run_kernel"
     if "crc32c_batch_kernel" in name:
         return name.replace("void ", "").replace("lnl::(anonymous namespace)::", "").split("(")[0]
     if name.startswith("stream_read"):

@@ -25,6 +25,10 @@ VARIANTS = {
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
     "k16": "-DLNL_RUN_K=16",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
+    "run_sc0": "-DLNL_RUN_AUX=1",
+    "run_sc0nt": "-DLNL_RUN_AUX=3",
+    "run_sc1": "-DLNL_RUN_AUX=16",
+    "run_sc1nt": "-DLNL_RUN_AUX=18",
     "dflt": "-DLNL_GLDS_AUX=0",                     # default cache policy
     "nocomp": "-DLNL_DIAG_NO_COMPUTE",              # memory-pipeline ceiling (wrong CRCs)
     "nocomp_dflt": "-DLNL_DIAG_NO_COMPUTE -DLNL_GLDS_AUX=0",
