@@ -122,6 +122,42 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
     return 0;
 }
 
+// CSR / verify batches: bucket the datagrams by line count first (crc32c_bucket.hip)
+// so that every wave's lanes need the same number of rows.  The permutation
+// lives in stream-ordered scratch (hipMallocAsync / hipFreeAsync on `st`), so
+// concurrent calls on different streams never share it.  Small batches skip
+// the pre-pass (its fixed cost would dominate).
+#ifndef LNL_BUCKET_MIN_N
+#define LNL_BUCKET_MIN_N 16384
+#endif
+int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
+    if (a.n < LNL_BUCKET_MIN_N) return launch(S, a, mode, st);
+    void* scratch = nullptr;
+    const size_t bytes = (2 * lnl::kBuckets + (size_t)a.n) * sizeof(uint32_t);
+    hipError_t e = hipMallocAsync(&scratch, bytes, st);
+    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
+    lnl::BucketArgs b{};
+    b.base = a.base;
+    b.off = a.off;
+    b.off0 = a.off0;
+    b.n = a.n;
+    b.verify = mode == lnl::kModeVerify;
+    b.counts = (uint32_t*)scratch;
+    b.fill = b.counts + lnl::kBuckets;
+    b.perm = b.fill + lnl::kBuckets;
+    e = lnl::launch_csr_buckets(b, st);
+    int rc = 0;
+    if (e != hipSuccess) {
+        rc = hip_fail(e, "bucket pre-pass launch");
+    } else {
+        a.perm = b.perm;
+        rc = launch(S, a, mode, st);
+    }
+    e = hipFreeAsync(scratch, st);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
+}
+
 // Lane-run plan for a fixed-stride batch (crc32c_run.hip): how many leading
 // datagrams the run kernel covers.  0 = use the batch kernel for all.
 #ifndef LNL_RUN_K
@@ -206,7 +242,7 @@ extern "C" int lnl_crc32c_batch_csr_dev(const uint8_t* d_base, const uint64_t* d
     a.off = d_off;
     a.n = n;
     a.out = d_out;
-    return launch(*S, a, lnl::kModeCsr, (hipStream_t)hip_stream);
+    return launch_csr(*S, a, lnl::kModeCsr, (hipStream_t)hip_stream);
 }
 
 extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
@@ -222,7 +258,7 @@ extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* 
     a.n = n;
     a.out = d_crc;
     a.ok = d_ok;
-    return launch(*S, a, lnl::kModeVerify, (hipStream_t)hip_stream);
+    return launch_csr(*S, a, lnl::kModeVerify, (hipStream_t)hip_stream);
 }
 
 // Host-resident batch: chunks of whole datagrams alternate over two streams;
@@ -308,7 +344,7 @@ extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_of
         a.off0 = h_off[i];
         a.n = cn;
         a.out = S->d_out[k];
-        if (int rc = launch(*S, a, lnl::kModeCsr, st)) return rc;
+        if (int rc = launch_csr(*S, a, lnl::kModeCsr, st)) return rc;
         if ((e = hipMemcpyAsync(h_out + i, S->d_out[k], (size_t)cn * 4, hipMemcpyDeviceToHost, st)) !=
             hipSuccess)
             return hip_fail(e, "D2H");

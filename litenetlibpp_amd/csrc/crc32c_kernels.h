@@ -22,6 +22,7 @@ struct BatchArgs {
     uint8_t* ok;           // Verify mode: 1 = trailing CRC matches
     const uint8_t* dummy;  // 16 readable bytes (library scratch) for idle glds lanes
     const uint32_t* fold;  // LNL_TABLE_WORDS words from lnl_build_tables (device)
+    const uint32_t* perm;  // optional: lane datagrams perm[64 b + lane] (CSR buckets)
 };
 
 // Enqueue one batch kernel on `stream` with `grid` workgroups.
@@ -43,5 +44,22 @@ struct RunArgs {
 };
 
 hipError_t launch_crc32c_run(const RunArgs& a, int grid, hipStream_t stream);
+
+// CSR pre-pass (crc32c_bucket.hip): perm[] = datagrams grouped by the number
+// of 128-byte lines they touch.  counts and fill: 2 * kBuckets words of
+// device scratch (zeroed by the launch).
+constexpr int kBuckets = 64;
+struct BucketArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    uint64_t off0;
+    uint32_t n;
+    uint32_t verify;  // verify mode: the CRC covers all but the last 4 bytes
+    uint32_t* counts;
+    uint32_t* fill;   // counts + kBuckets
+    uint32_t* perm;   // n entries
+};
+
+hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream);
 
 }  // namespace lnl

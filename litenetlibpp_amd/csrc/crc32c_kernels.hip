@@ -135,7 +135,11 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
     B.valid = uni(b < nbatch ? 1u : 0u);
     uint64_t start;
     uint32_t len;
-    B.p = B.valid ? b * 64u + lane : a.n;
+    {
+        const uint32_t idx = b * 64u + lane;
+        const bool real = B.valid && idx < a.n;
+        B.p = real ? (a.perm ? a.perm[idx] : idx) : a.n;
+    }
     lane_extent<kMode>(a, B.p, start, len);
     const uint64_t abs0 = (uint64_t)(uintptr_t)a.base + start;
     const uint64_t abs1 = abs0 + len - 1u;  // last byte (unused when len == 0)

@@ -197,3 +197,35 @@ void oracle_batch_csr_bitwise(const uint8_t *base, const uint64_t *off, uint64_t
     for (uint64_t i = 0; i < n; ++i)
         out[i] = oracle_crc32c_bitwise(base + off[i], (size_t)(off[i + 1] - off[i]));
 }
+
+/* ---- SURVEY.md section 8(d) synthetic input --------------------------------
+ * mt19937_64 (Matsumoto & Nishimura 2000; the standard C++ engine: n = 312,
+ * m = 156, matrix 0xB5026F5AA96619E9, tempering u=29 d=0x5555555555555555
+ * s=17 b=0x71D67FFFEDA60000 t=37 c=0xFFF7EEE000000000 l=43, seeding with
+ * 6364136223846793005) outputs stored little-endian: the recipe SURVEY.md
+ * pins with out[0] = CRC-32C(first 1400 bytes of seed 42) = 0xD26C5CFE. */
+void oracle_fill_mt19937_64(uint64_t seed, uint64_t *out, size_t nwords)
+{
+    uint64_t mt[312];
+    mt[0] = seed;
+    for (int i = 1; i < 312; ++i)
+        mt[i] = 6364136223846793005ull * (mt[i - 1] ^ (mt[i - 1] >> 62)) + (uint64_t)i;
+    int idx = 312;
+    for (size_t k = 0; k < nwords; ++k) {
+        if (idx >= 312) {
+            for (int i = 0; i < 312; ++i) {
+                const uint64_t x = (mt[i] & 0xFFFFFFFF80000000ull) | (mt[(i + 1) % 312] & 0x7FFFFFFFull);
+                uint64_t xa = x >> 1;
+                if (x & 1u) xa ^= 0xB5026F5AA96619E9ull;
+                mt[i] = mt[(i + 156) % 312] ^ xa;
+            }
+            idx = 0;
+        }
+        uint64_t y = mt[idx++];
+        y ^= (y >> 29) & 0x5555555555555555ull;
+        y ^= (y << 17) & 0x71D67FFFEDA60000ull;
+        y ^= (y << 37) & 0xFFF7EEE000000000ull;
+        y ^= y >> 43;
+        out[k] = y; /* x86-64 / gfx950 hosts are little-endian */
+    }
+}

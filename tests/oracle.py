@@ -46,6 +46,16 @@ def load():
     return L
 
 
+def mt19937_64_bytes(seed: int, nbytes: int) -> np.ndarray:
+    """SURVEY.md 8(d) synthetic input: mt19937_64(seed) outputs, little-endian."""
+    words = np.empty((nbytes + 7) // 8, dtype=np.uint64)
+    L = load()
+    L.oracle_fill_mt19937_64.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]
+    L.oracle_fill_mt19937_64.restype = None
+    L.oracle_fill_mt19937_64(seed, words.ctypes.data, words.size)
+    return words.view(np.uint8)[:nbytes]
+
+
 def _buf(b):
     arr = np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray) else np.ascontiguousarray(b)
     return arr

@@ -148,6 +148,69 @@ def test_csr_mixed_length_config3_shape(P):
     assert np.array_equal(got, exp)
 
 
+def test_csr_bucketed_mix(P):
+    """Batches large enough for the line-count bucketing pre-pass
+    (crc32c_bucket.hip): empty, 1..3-byte, line-crossing and very long
+    datagrams (line-count bucket 63) mixed, buffer not line-aligned."""
+    rng = np.random.default_rng(21)
+    n = 40000
+    lens = rng.integers(0, 1433, n)
+    lens[rng.integers(0, n, 3000)] = 0
+    lens[rng.integers(0, n, 3000)] = rng.integers(1, 4, 3000)
+    lens[rng.integers(0, n, 20)] = rng.integers(8000, 70000, 20)
+    lead = 77
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(lead)
+    data = rng.integers(0, 256, int(off[-1]) + 9, dtype=np.uint8)
+    exp = oracle.batch_csr(data, off)
+    d = dev(np.concatenate([np.zeros(5, np.uint8), data]))[5:]
+    got = u32(P.batch_csr(d, dev(off.view(np.int64), torch.int64)))
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+
+
+def test_verify_mode_bucketed(P):
+    rng = np.random.default_rng(22)
+    n = 30000
+    lens = rng.integers(0, 1433, n)
+    lens[::13] = rng.integers(0, 5, lens[::13].size)   # runts
+    body_off = np.concatenate([[0], np.cumsum(lens + 4)])[:-1].astype(np.uint64)
+    wire = np.empty(int(np.sum(lens + 4)), np.uint8)
+    bodies = rng.integers(0, 256, int(np.sum(lens)), dtype=np.uint8)
+    boff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    crcs = oracle.batch_csr(bodies, boff)
+    for i in range(n):
+        o, L = int(body_off[i]), int(lens[i])
+        wire[o:o + L] = bodies[int(boff[i]):int(boff[i]) + L]
+        wire[o + L:o + L + 4] = np.frombuffer(int(crcs[i]).to_bytes(4, "little"), np.uint8)
+    corrupt = rng.integers(0, n, 500)
+    for i in corrupt:
+        o, L = int(body_off[i]), int(lens[i]) + 4
+        wire[o + int(rng.integers(0, L))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    off = np.concatenate([body_off, [wire.size]]).astype(np.uint64)
+    want = np.zeros(n, bool)
+    tot = lens + 4
+    for i in range(n):
+        o, T = int(off[i]), int(tot[i])
+        if T >= 5:
+            want[i] = oracle.crc(wire[o:o + T - 4]) == int.from_bytes(wire[o + T - 4:o + T].tobytes(), "little")
+    ok, _ = P.verify_csr(dev(wire), dev(off.view(np.int64), torch.int64), want_crc=True)
+    assert np.array_equal(ok.cpu().numpy().astype(bool), want)
+
+
+def test_full_config3_bit_exact(P):
+    # BASELINE config 3 at full size: 2^20 datagrams of 64..1400 B, CSR
+    rng = np.random.default_rng(43)
+    lens = 64 + rng.integers(0, 1337, 1 << 20)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(44)
+    d = torch.randint(0, 256, (int(off[-1]),), dtype=torch.uint8, device="cuda", generator=g)
+    got = u32(P.batch_csr(d, dev(off.view(np.int64), torch.int64)))
+    exp = oracle.batch_csr(d.cpu().numpy(), off)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+
+
 def test_csr_empty_datagrams_and_all_empty_batches(P):
     rng = np.random.default_rng(7)
     lens = np.zeros(300, np.int64)
@@ -252,6 +315,17 @@ def test_full_config2_bit_exact(P):
     # size-independent property: checksum of checksums is stable across launches
     again = u32(P.batch_fixed(data, L, L, n))
     assert np.array_equal(got, again)
+
+
+def test_full_config2_survey_input(P):
+    # SURVEY.md 8(d) recipe: mt19937_64(42) bytes; pinned out[0] = 0xD26C5CFE
+    n, L = 1 << 20, 1400
+    host = oracle.mt19937_64_bytes(42, n * L)
+    got = u32(P.batch_fixed(dev(host), L, L, n))
+    assert got[0] == 0xD26C5CFE
+    exp = oracle.batch_fixed(host, L, L, n)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
 
 
 def test_error_paths_raise(P):

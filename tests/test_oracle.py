@@ -79,3 +79,14 @@ def test_golden_fixed():
     data = np.fromfile(os.path.join(GOLD, "fixed_bytes.bin"), dtype=np.uint8)
     exp = np.fromfile(os.path.join(GOLD, "fixed_crc.u32"), dtype=np.uint32)
     assert np.array_equal(oracle.batch_fixed(data, 1400, 1400, 64), exp)
+
+
+def test_survey_config2_pin():
+    """config 2's synthetic bytes are mt19937_64(42) outputs
+    stored little-endian, and the first 1400-byte datagram's CRC-32C is
+    0xD26C5CFE (computed there with an independent C++ implementation)."""
+    b = oracle.mt19937_64_bytes(42, 3 * 1400)
+    assert oracle.crc(b[:1400]) == 0xD26C5CFE
+    assert oracle.crc(b[:1400], "bitwise") == 0xD26C5CFE
+    assert oracle.crc(b[:1400], "sliced") == 0xD26C5CFE
+
