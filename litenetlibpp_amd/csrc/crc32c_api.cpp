@@ -114,6 +114,13 @@ int grid_for(const DeviceState& S, uint32_t n) {
     return (int)std::max(1u, std::min(wgs, cap));
 }
 
+int grid_for_waves(const DeviceState& S, uint32_t waves) {
+    const uint32_t per_wg = lnl::kBlockThreads / 64;
+    const uint32_t wgs = (waves + per_wg - 1) / per_wg;
+    const uint32_t cap = (uint32_t)S.cus * (uint32_t)(lnl::kWavesPerCU / per_wg);
+    return (int)std::max(1u, std::min(wgs, cap));
+}
+
 int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
     a.dummy = S.dummy;
     a.fold = S.fold;
@@ -130,7 +137,50 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
 #ifndef LNL_BUCKET_MIN_N
 #define LNL_BUCKET_MIN_N 16384
 #endif
+#ifndef LNL_PAIR_MIN_N
+#define LNL_PAIR_MIN_N 16384
+#endif
+// CSR batches: the pair kernel (crc32c_pair.hip) after its bucket pre-pass;
+// pairs with very long datagrams go to the batch kernel (device-side count).
+int launch_csr_pairs(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
+    void* scratch = nullptr;
+    const size_t bytes = lnl::pair_prep_scratch_words(a.n) * sizeof(uint32_t);
+    hipError_t e = hipMallocAsync(&scratch, bytes, st);
+    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
+    lnl::PairPrepArgs p{};
+    p.base = a.base;
+    p.off = a.off;
+    p.off0 = a.off0;
+    p.n = a.n;
+    lnl::pair_prep_layout(p, (uint32_t*)scratch);
+    int rc = 0;
+    e = lnl::launch_pair_prep(p, st);
+    if (e != hipSuccess) rc = hip_fail(e, "pair pre-pass launch");
+    if (rc == 0) {
+        lnl::PairArgs q{};
+        q.base = a.base;
+        q.n = a.n;
+        q.out = a.out;
+        q.fold = S.fold;
+        q.desc = p.desc;
+        q.nwb = p.ctl;
+        const uint32_t waves_max = (a.n / 2u + 1u) / 64u + 1u + lnl::kPairKeys;
+        e = lnl::launch_crc32c_pair(q, grid_for_waves(S, waves_max), st);
+        if (e != hipSuccess) rc = hip_fail(e, "pair kernel launch");
+    }
+    if (rc == 0) {
+        lnl::BatchArgs o = a;
+        o.perm = p.ovf;
+        o.perm_n = p.ctl + 1;
+        rc = launch(S, o, lnl::kModeCsr, st);
+    }
+    e = hipFreeAsync(scratch, st);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
+}
+
 int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
+    if (mode == lnl::kModeCsr && a.n >= LNL_PAIR_MIN_N) return launch_csr_pairs(S, a, st);
     if (a.n < LNL_BUCKET_MIN_N) return launch(S, a, mode, st);
     void* scratch = nullptr;
     const size_t bytes = (2 * lnl::kBuckets + (size_t)a.n) * sizeof(uint32_t);
@@ -186,12 +236,6 @@ uint32_t run_plan(size_t stride, uint32_t len, uint32_t n, lnl::RunArgs& r) {
     return n_main;
 }
 
-int grid_for_waves(const DeviceState& S, uint32_t waves) {
-    const uint32_t per_wg = lnl::kBlockThreads / 64;
-    const uint32_t wgs = (waves + per_wg - 1) / per_wg;
-    const uint32_t cap = (uint32_t)S.cus * (uint32_t)(lnl::kWavesPerCU / per_wg);
-    return (int)std::max(1u, std::min(wgs, cap));
-}
 
 }  // namespace
 

@@ -213,3 +213,22 @@ LNL_HD LNL_INLINE void lnl_fold_pair(const uint32_t* a, const uint32_t* b, uint3
     ra = x;
     rb = y;
 }
+
+// A level-1 fold result is meaningful at even bits only, so two of its words
+// fit in one: p[m] = f[2m] (even bits) | f[2m+1] (moved to the odd bits).
+// The pair kernel keeps the first datagram's result like this (16 registers,
+// not 32) until its partner's is ready.
+LNL_HD LNL_INLINE void lnl_pack_level1(const uint32_t* f, uint32_t* p) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) p[m] = (f[2 * m] & 0x55555555u) | ((f[2 * m + 1] << 1) & 0xAAAAAAAAu);
+}
+
+LNL_HD LNL_INLINE void lnl_fold_pair_packed(const uint32_t* p, const uint32_t* b, uint32_t& ra, uint32_t& rb) {
+    uint32_t a[32];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        a[2 * m] = p[m] & 0x55555555u;
+        a[2 * m + 1] = (p[m] >> 1) & 0x55555555u;
+    }
+    lnl_fold_pair(a, b, ra, rb);
+}

@@ -74,6 +74,16 @@ __device__ LNL_INLINE void patch_piece(uint32_t addr, const uint32_t* m) {
     asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
 }
 
+// One 16-byte LDS piece read / written (asm, see read_row).
+__device__ LNL_INLINE u32x4 lds_read_piece(uint32_t addr) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+__device__ LNL_INLINE void lds_write_piece(uint32_t addr, u32x4 v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
 // One fold matrix applied to v: 8 nibble lookups in the LDS copy of the fold
 // tables (inline asm for the same reason as read_row).
 __device__ LNL_INLINE uint32_t fold_apply_lds(uint32_t mat_base, uint32_t v) {

@@ -23,6 +23,7 @@ struct BatchArgs {
     const uint8_t* dummy;  // 16 readable bytes (library scratch) for idle glds lanes
     const uint32_t* fold;  // LNL_TABLE_WORDS words from lnl_build_tables (device)
     const uint32_t* perm;  // optional: lane datagrams perm[64 b + lane] (CSR buckets)
+    const uint32_t* perm_n;  // optional (device): number of perm entries, else n
 };
 
 // Enqueue one batch kernel on `stream` with `grid` workgroups.
@@ -61,5 +62,48 @@ struct BucketArgs {
 };
 
 hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream);
+
+// CSR pair kernel (crc32c_pair.hip) and its pre-pass.  Item j = datagrams
+// (2j, 2j+1); key = (Ta, Tb, shared) with Ta, Tb <= kPairMaxT, else overflow
+// (both datagrams go to the batch kernel through `ovf`).  perm lists items
+// key by key, each key's group padded with kPairIdle to a multiple of 64.
+constexpr uint32_t kPairMaxT = 15;
+constexpr uint32_t kPairKeys = (kPairMaxT + 1) * (kPairMaxT + 1) * 2;  // 512
+constexpr uint32_t kPairIdle = 0xFFFFFFFFu;
+
+struct PairPrepArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    uint64_t off0;
+    uint32_t n;         // datagrams; items = (n + 1) / 2
+    uint32_t* counts;   // kPairKeys + 1 (last: overflow items)
+    uint32_t* fill;     // kPairKeys
+    uint32_t* bases;    // kPairKeys: start of each key's group in perm
+    uint32_t* ctl;      // [0] = wave-batches (desc entries / 64), [1] = overflow datagrams
+    uint4* desc;        // items + 64 * kPairKeys pair descriptors (see PairArgs)
+    uint32_t* ovf;      // n entries
+};
+
+// Zeroes the counters, then count / bases+padding / scatter kernels.
+hipError_t launch_pair_prep(const PairPrepArgs& a, hipStream_t stream);
+size_t pair_prep_scratch_words(uint32_t n);
+void pair_prep_layout(PairPrepArgs& a, uint32_t* scratch);
+
+// Pair descriptor, written by the pre-pass in bucket order, one per lane:
+//   x: line index of the run's first line, counted from base's line
+//   y: pad_a | be_a << 8 | pad_b << 16 | be_b << 24 (offsets of a's / b's
+//      first and last byte in their first / last line)
+//   z: datagram a (b = a + 1); n marks a padding (idle) entry
+//   w: (b < n) | key << 8, key = (Ta * (kPairMaxT + 1) + Tb) * 2 + shared
+struct PairArgs {
+    const uint8_t* base;
+    uint32_t n;
+    uint32_t* out;
+    const uint32_t* fold;
+    const uint4* desc;
+    const uint32_t* nwb;  // device: wave-batches
+};
+
+hipError_t launch_crc32c_pair(const PairArgs& a, int grid, hipStream_t stream);
 
 }  // namespace lnl

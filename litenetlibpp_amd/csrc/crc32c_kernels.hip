@@ -93,6 +93,12 @@ struct Batch {
     // first_q | head piece hp_q << 20 | tail piece tp_q << 23 | idle << 30
     uint64_t ladr[8];
     uint32_t lfirst[8];
+    // uniform: every lane busy and starting at row 0 (the common case once CSR
+    // batches are bucketed by line count): the only edge rows are 0 and rows-1
+    uint32_t uedge;
+    // load lanes, uedge batches: bit i = fetch piece of glds i on the head row,
+    // bit 8 + i = on the tail row (else the zero line)
+    uint32_t ebits;
 };
 
 template <int kMode>
@@ -127,8 +133,8 @@ __device__ LNL_INLINE uint32_t wave_max(uint32_t v) {
 }
 
 template <int kMode>
-__device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t nbatch, uint32_t tab_base,
-                                      Batch& B) {
+__device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t nbatch, uint32_t nperm,
+                                      uint32_t tab_base, Batch& B) {
     // Branch-free on purpose (every field written on every path keeps the
     // struct in registers).  An invalid batch (b >= nbatch) has only idle lanes.
     const uint32_t lane = __lane_id();
@@ -137,7 +143,7 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
     uint32_t len;
     {
         const uint32_t idx = b * 64u + lane;
-        const bool real = B.valid && idx < a.n;
+        const bool real = B.valid && idx < nperm;
         B.p = real ? (a.perm ? a.perm[idx] : idx) : a.n;
     }
     lane_extent<kMode>(a, B.p, start, len);
@@ -165,6 +171,16 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
         B.ladr[i] = (((uint64_t)hi << 32) | lo) + 16u * (slot ^ swz(q));
         B.lfirst[i] = (uint32_t)__shfl((int)fl, q, 64);
     }
+    B.uedge = uni(B.simple && B.max_first == 0u ? 1u : 0u);
+    uint32_t eb = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t f = B.lfirst[i];
+        const uint32_t piece = slot ^ swz(8u * i + sub);
+        eb |= (piece >= ((f >> 20) & 7u) ? 1u : 0u) << i;
+        eb |= (piece <= ((f >> 23) & 7u) ? 1u : 0u) << (8 + i);
+    }
+    B.ebits = eb;
 }
 
 // Issue the 8 LDS-DMA instructions that bring row t of batch B into `buf`.
@@ -180,6 +196,15 @@ __device__ LNL_INLINE void issue_row(const BatchArgs& a, const Batch& B, uint32_
         for (int i = 0; i < 8; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(B.ladr[i] + dt),
                                              (void*)(buf + 64 * i), 16, 0, LNL_GLDS_AUX);
+    } else if (B.uedge) {
+        // rows 0 and rows-1 of a batch whose lanes all start at row 0
+        const uint32_t m = (t == 0u ? B.ebits : 0xFFu) & (t + 1u == B.rows ? (B.ebits >> 8) : 0xFFu);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t src = (m >> i) & 1u ? B.ladr[i] + dt : (uint64_t)(uintptr_t)a.dummy;
+            __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (void*)(buf + 64 * i), 16,
+                                             0, LNL_EDGE_AUX);
+        }
     } else {
         const bool last = t + 1u == B.rows;
 #pragma unroll
@@ -226,14 +251,17 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
     uint4* const fold_lds = lds + kWaves * 2 * kBufU4;
     const uint32_t fold_base = (uint32_t)(uintptr_t)fold_lds;
 
+    // entries to process: n, or a device-side count of perm entries
+    const uint32_t nperm = a.perm_n ? uni(*a.perm_n) : a.n;
+    const uint32_t nbatch = (nperm + 63u) >> 6;
+    if (blockIdx.x * kWaves >= nbatch) return;  // whole workgroup idle (before the barrier)
+
     // stage the tables (before any LDS-DMA is in flight)
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.fold);
         for (int i = threadIdx.x; i < kFoldU4; i += kBlockThreads) fold_lds[i] = g[i];
         __syncthreads();
     }
-
-    const uint32_t nbatch = (a.n + 63u) >> 6;
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint32_t nw = gridDim.x * kWaves;
 
@@ -247,9 +275,9 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
 
     Batch cur, nxt;
     uint32_t b = gw;
-    make_batch<kMode>(a, b, nbatch, fold_base, cur);
+    make_batch<kMode>(a, b, nbatch, nperm, fold_base, cur);
     if (!cur.valid) return;
-    make_batch<kMode>(a, b + nw, nbatch, fold_base, nxt);
+    make_batch<kMode>(a, b + nw, nbatch, nperm, fold_base, nxt);
 
     // Row pipeline.  `step` counts computed rows; row `step` lives in buffer
     // step & 1.  have0: row `step` has been issued; have1: row step+1 has been
@@ -280,7 +308,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
             b += nw;
             cur = nxt;
             if (!cur.valid) break;
-            make_batch<kMode>(a, b + nw, nbatch, fold_base, nxt);
+            make_batch<kMode>(a, b + nw, nbatch, nperm, fold_base, nxt);
             have0 = 0;  // nothing can have been issued for it
             have1 = 0;
             continue;
@@ -374,7 +402,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
             b += nw;
             cur = nxt;
             if (!cur.valid) break;
-            make_batch<kMode>(a, b + nw, nbatch, fold_base, nxt);
+            make_batch<kMode>(a, b + nw, nbatch, nperm, fold_base, nxt);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

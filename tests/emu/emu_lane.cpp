@@ -155,6 +155,85 @@ static int check_runs(const std::vector<uint8_t>& mem, int& checked) {
     return bad;
 }
 
+// One lane of the CSR pair kernel (crc32c_pair.hip): datagrams a = [sa, sa+la)
+// and b = [sa+la, sa+la+lb) (CSR datagrams are contiguous) as Ta + Tb steps,
+// step u reading line u (u < Ta) or u - shared (u >= Ta) of the run -- the
+// line a and b share is read at two consecutive steps -- framed at read time
+// to bytes lo..hi (a's / b's first byte on its first step, last byte on its
+// last step); a fresh state V = X on a datagram's first step; pairwise fold.
+static void pair_lane(const uint8_t* mem, size_t sa, uint32_t la, uint32_t lb, uint32_t* ca, uint32_t* cb) {
+    const size_t sb = sa + la;
+    const uint32_t Ta = la ? (uint32_t)(((sa + la - 1) >> 7) - (sa >> 7) + 1) : 0;
+    const uint32_t Tb = lb ? (uint32_t)(((sb + lb - 1) >> 7) - (sb >> 7) + 1) : 0;
+    const uint32_t shared = (la && lb && ((sa + la - 1) >> 7) == (sb >> 7)) ? 1u : 0u;
+    const uint32_t steps = Ta + Tb;
+    *ca = 0;
+    *cb = 0;
+    if (steps == 0) return;
+    const size_t first = la ? sa : sb;
+    const size_t line0 = first & ~(size_t)127;
+    const uint32_t pad_a = (uint32_t)(sa & 127), be_a = (uint32_t)((sa + la - 1) & 127);
+    const uint32_t pad_b = (uint32_t)(sb & 127), be_b = (uint32_t)((sb + lb - 1) & 127);
+    uint32_t s[32] = {0}, P[16] = {0};
+    for (uint32_t u = 0; u < steps; ++u) {
+        const uint32_t line = u - (shared && u >= Ta ? 1u : 0u);
+        uint32_t x[32];
+        memcpy(x, mem + line0 + 128 * (size_t)line, 128);
+        const bool inA = u < Ta;
+        const bool start = u == 0 || u == Ta;
+        const bool end = u + 1 == Ta || u + 1 == steps;
+        const uint32_t lo = start ? (inA ? pad_a : pad_b) : 0u;
+        const uint32_t hi = end ? (inA ? be_a : be_b) : 127u;
+        for (int w = 0; w < 32; ++w) x[w] &= lnl_word_keep_ge(w, lo) & lnl_word_keep_le(w, hi);
+        if (start) {
+            x[0] ^= g_tab[LNL_TABLE_C_OFF + (inA ? pad_a : pad_b)];
+            memcpy(s, x, sizeof s);
+        } else {
+            uint32_t o[32];
+            lnl_net_row_x(s, x, o);
+            memcpy(s, o, sizeof s);
+        }
+        if (end) {
+            if (inA) {
+                uint32_t fa[32];
+                lnl_fold_level1(s, fa);
+                lnl_pack_level1(fa, P);
+            }
+            if (!inA || !Tb) {
+                uint32_t f[32] = {0}, ra, rb;
+                if (!inA) lnl_fold_level1(s, f);
+                lnl_fold_pair_packed(P, f, ra, rb);
+                const uint32_t ea = 127u - be_a, eb = 127u - be_b;
+                if (Ta) *ca = ~lnl_table_apply(g_tab + 128 * lnl_table_a(ea), lnl_table_apply(g_tab + 128 * lnl_table_b(ea), ra));
+                if (Tb) *cb = ~lnl_table_apply(g_tab + 128 * lnl_table_a(eb), lnl_table_apply(g_tab + 128 * lnl_table_b(eb), rb));
+            }
+        }
+    }
+}
+
+static int check_pairs(const std::vector<uint8_t>& mem, int& checked) {
+    int bad = 0;
+    std::mt19937_64 rng(99);
+    const uint32_t lens[] = {0, 1, 2, 3, 4, 15, 16, 17, 100, 126, 127, 128, 129, 200, 255, 256, 257, 700, 1400, 1432, 3000};
+    for (uint32_t la : lens)
+        for (uint32_t lb : lens)
+            for (int rep = 0; rep < 6; ++rep) {
+                const size_t sa = 4096 + (rng() % 128) + (rep == 0 ? 0 : 128 * (rng() % 4));
+                uint32_t ca, cb;
+                pair_lane(mem.data(), sa, la, lb, &ca, &cb);
+                const uint32_t ea = oracle_crc32c_hw(mem.data() + sa, la);
+                const uint32_t eb = oracle_crc32c_hw(mem.data() + sa + la, lb);
+                checked += 2;
+                if (ca != ea || cb != eb) {
+                    if (bad < 20)
+                        printf("PAIR MISMATCH la=%u lb=%u sa=%zu got=%08x,%08x exp=%08x,%08x\n", la, lb, sa, ca, cb,
+                               ea, eb);
+                    ++bad;
+                }
+            }
+    return bad;
+}
+
 int main(int argc, char** argv) {
     const int max_len = argc > 1 ? atoi(argv[1]) : 1500;
     lnl_build_tables(g_tab);
@@ -185,6 +264,7 @@ int main(int argc, char** argv) {
         }
     }
     bad += check_runs(mem, checked);
+    bad += check_pairs(mem, checked);
     printf("checked=%d bad=%d\n", checked, bad);
     return bad ? 1 : 0;
 }

@@ -168,6 +168,32 @@ def test_csr_bucketed_mix(P):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
 
 
+@pytest.mark.parametrize("case", ["odd_n", "tiny", "line_multiples", "overflow_heavy"])
+def test_csr_pairs(P, case):
+    """CSR pair kernel (crc32c_pair.hip): a lone last datagram (odd n), pairs of
+    tiny datagrams sharing one line, lengths that end exactly on line
+    boundaries (unshared pairs), and many pairs too long for the pair buckets
+    (the batch-kernel overflow path)."""
+    rng = np.random.default_rng(["odd_n", "tiny", "line_multiples", "overflow_heavy"].index(case) + 300)
+    n = {"odd_n": 30001, "tiny": 50000, "line_multiples": 20000, "overflow_heavy": 20000}[case]
+    if case == "tiny":
+        lens = rng.integers(0, 12, n)
+    elif case == "line_multiples":
+        lens = 128 * rng.integers(0, 12, n) + rng.choice([0, 0, 0, 1, 127], n)
+    elif case == "overflow_heavy":
+        lens = rng.integers(0, 1433, n)
+        lens[rng.integers(0, n, n // 8)] = rng.integers(1900, 4000, n // 8)
+    else:
+        lens = rng.integers(0, 1433, n)
+    lead = int(rng.integers(0, 128))
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(lead)
+    data = rng.integers(0, 256, int(off[-1]) + 3, dtype=np.uint8)
+    exp = oracle.batch_csr(data, off)
+    got = u32(P.batch_csr(dev(data), dev(off.view(np.int64), torch.int64)))
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{case}: {bad.size} mismatches, first at {bad[:5]}"
+
+
 def test_verify_mode_bucketed(P):
     rng = np.random.default_rng(22)
     n = 30000

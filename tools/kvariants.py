@@ -25,6 +25,8 @@ VARIANTS = {
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
     "k16": "-DLNL_RUN_K=16",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
+    "nobucket": "-DLNL_BUCKET_MIN_N=0xFFFFFFFFu -DLNL_PAIR_MIN_N=0xFFFFFFFFu",  # CSR: plain batch kernel
+    "nopair": "-DLNL_PAIR_MIN_N=0xFFFFFFFFu",       # CSR: bucketed batch kernel instead of the pair kernel
     "run_sc0": "-DLNL_RUN_AUX=1",
     "run_sc0nt": "-DLNL_RUN_AUX=3",
     "run_sc1": "-DLNL_RUN_AUX=16",
@@ -53,33 +55,53 @@ def run(names, rounds, workloads):
         L = ctypes.CDLL(os.path.join(VDIR, n + ".so"))
         L.lnl_crc32c_batch_fixed_dev.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
                                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        L.lnl_crc32c_batch_csr_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.c_void_p, ctypes.c_void_p]
         libs[n] = L
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(42)
     results = {}
-    for (n_pk, L_pk, stride, shift) in workloads:
-        buf = torch.randint(0, 256, (n_pk * stride + 256,), dtype=torch.uint8, device=dev, generator=g)
-        data = buf[shift:]
-        out = torch.empty(n_pk, dtype=torch.int32, device=dev)
+    for wl in workloads:
         s = torch.cuda.current_stream()
+        if wl[0] == "csr":  # ("csr", n, lmin, lmax): config-3-shaped CSR batch
+            _, n_pk, lmin, lmax = wl
+            lens = torch.randint(lmin, lmax + 1, (n_pk,), device=dev, generator=g, dtype=torch.int64)
+            off = torch.zeros(n_pk + 1, dtype=torch.int64, device=dev)
+            off[1:] = torch.cumsum(lens, 0)
+            total = int(off[-1])
+            data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+            out = torch.empty(n_pk, dtype=torch.int32, device=dev)
+            algo = total + 12 * n_pk + 8
+            wkey = f"csr{n_pk}x{lmin}-{lmax}"
+
+            def call(L):
+                L.lnl_crc32c_batch_csr_dev(data.data_ptr(), off.data_ptr(), n_pk, out.data_ptr(), s.cuda_stream)
+        else:
+            n_pk, L_pk, stride, shift = wl
+            buf = torch.randint(0, 256, (n_pk * stride + 256,), dtype=torch.uint8, device=dev, generator=g)
+            data = buf[shift:]
+            out = torch.empty(n_pk, dtype=torch.int32, device=dev)
+            algo = n_pk * (L_pk + 4)
+            wkey = f"{n_pk}x{L_pk}/s{stride}+{shift}"
+
+            def call(L):
+                L.lnl_crc32c_batch_fixed_dev(data.data_ptr(), stride, L_pk, n_pk, out.data_ptr(), s.cuda_stream)
         times = {n: [] for n in names}
         for r in range(rounds):
             for n in names:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
-                libs[n].lnl_crc32c_batch_fixed_dev(data.data_ptr(), stride, L_pk, n_pk, out.data_ptr(), s.cuda_stream)
+                call(libs[n])
                 e0.record(s)
                 for _ in range(3):
-                    libs[n].lnl_crc32c_batch_fixed_dev(data.data_ptr(), stride, L_pk, n_pk, out.data_ptr(),
-                                                       s.cuda_stream)
+                    call(libs[n])
                 e1.record(s)
                 torch.cuda.synchronize()
                 times[n].append(e0.elapsed_time(e1) / 3)
         for n in names:
             med = float(np.median(times[n]))
-            algo = n_pk * (L_pk + 4)
-            key = f"{n}@{n_pk}x{L_pk}/s{stride}+{shift}"
+            key = f"{n}@{wkey}"
             results[key] = {"us": round(med * 1e3, 2), "min_us": round(min(times[n]) * 1e3, 2),
                             "GBps": round(algo / (med * 1e-3) / 1e9, 1)}
             print(key, results[key], flush=True)
@@ -91,15 +113,16 @@ def main():
     ap.add_argument("cmd", choices=["build", "run"])
     ap.add_argument("--names", default=",".join(VARIANTS))
     ap.add_argument("--rounds", type=int, default=10)
-    ap.add_argument("--workloads", default="1048576:1400:1400:0,1048576:1408:1408:0",
-                    help="n:len:stride:byte_shift,...")
+    ap.add_argument("--workloads", default="1048576:1400:1400:0,csr:1048576:64:1400",
+                    help="n:len:stride:byte_shift or csr:n:min_len:max_len, comma-separated")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "kvariants.json"))
     a = ap.parse_args()
     names = a.names.split(",")
     if a.cmd == "build":
         build(names)
     else:
-        wl = [tuple(int(v) for v in w.split(":")) for w in a.workloads.split(",")]
+        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.startswith("csr")
+              else tuple(int(v) for v in w.split(":")) for w in a.workloads.split(",")]
         res = run(names, a.rounds, wl)
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
         with open(a.out, "w") as f:
