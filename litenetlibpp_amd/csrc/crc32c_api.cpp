@@ -302,7 +302,31 @@ extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* 
     a.n = n;
     a.out = d_crc;
     a.ok = d_ok;
-    return launch_csr(*S, a, lnl::kModeVerify, (hipStream_t)hip_stream);
+    hipStream_t st = (hipStream_t)hip_stream;
+    if (n < LNL_PAIR_MIN_N) return launch_csr(*S, a, lnl::kModeVerify, st);
+    // large batches: CRCs of the whole wire datagrams with the pair kernel,
+    // then ok / body CRC per datagram (crc32c_verify.hip)
+    void* wire = nullptr;
+    hipError_t e = hipMallocAsync(&wire, (size_t)n * 4u, st);
+    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync: %s", hipGetErrorString(e));
+    lnl::BatchArgs w = a;
+    w.out = (uint32_t*)wire;
+    w.ok = nullptr;
+    int rc = launch_csr_pairs(*S, w, st);
+    if (rc == 0) {
+        lnl::VerifyArgs v{};
+        v.base = d_base;
+        v.off = d_off;
+        v.n = n;
+        v.wire = (const uint32_t*)wire;
+        v.ok = d_ok;
+        v.crc = d_crc;
+        e = lnl::launch_verify_from_wire(v, st);
+        if (e != hipSuccess) rc = hip_fail(e, "verify epilogue launch");
+    }
+    e = hipFreeAsync(wire, st);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
 }
 
 // Host-resident batch: chunks of whole datagrams alternate over two streams;

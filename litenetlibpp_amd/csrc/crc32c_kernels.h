@@ -106,4 +106,17 @@ struct PairArgs {
 
 hipError_t launch_crc32c_pair(const PairArgs& a, int grid, hipStream_t stream);
 
+// Verify epilogue (crc32c_verify.hip): ok / body CRC from wire-datagram CRCs.
+struct VerifyArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    uint64_t off0;
+    uint32_t n;
+    const uint32_t* wire;  // CRC-32C of each whole datagram
+    uint8_t* ok;
+    uint32_t* crc;         // optional
+};
+
+hipError_t launch_verify_from_wire(const VerifyArgs& a, hipStream_t stream);
+
 }  // namespace lnl

@@ -214,13 +214,17 @@ def test_verify_mode_bucketed(P):
         wire[o + int(rng.integers(0, L))] ^= np.uint8(1 << int(rng.integers(0, 8)))
     off = np.concatenate([body_off, [wire.size]]).astype(np.uint64)
     want = np.zeros(n, bool)
+    want_crc = np.zeros(n, np.uint32)
     tot = lens + 4
     for i in range(n):
         o, T = int(off[i]), int(tot[i])
         if T >= 5:
-            want[i] = oracle.crc(wire[o:o + T - 4]) == int.from_bytes(wire[o + T - 4:o + T].tobytes(), "little")
-    ok, _ = P.verify_csr(dev(wire), dev(off.view(np.int64), torch.int64), want_crc=True)
+            want_crc[i] = oracle.crc(wire[o:o + T - 4])
+            want[i] = int(want_crc[i]) == int.from_bytes(wire[o + T - 4:o + T].tobytes(), "little")
+    ok, crc = P.verify_csr(dev(wire), dev(off.view(np.int64), torch.int64), want_crc=True)
     assert np.array_equal(ok.cpu().numpy().astype(bool), want)
+    big = tot >= 5
+    assert np.array_equal(u32(crc)[big], want_crc[big])
 
 
 def test_full_config3_bit_exact(P):
