@@ -137,8 +137,16 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
 #ifndef LNL_BUCKET_MIN_N
 #define LNL_BUCKET_MIN_N 16384
 #endif
+// The CSR pair kernel (crc32c_pair.hip) is an experiment, off by default: it
+// fetches 13 % fewer HBM bytes on config 3 than the bucketed batch kernel but
+// streams them at ~5.0 TB/s against ~6.1 TB/s, and its pre-pass is heavier
+// (0.233 vs 0.184 ms per config-3 batch).  Build with -DLNL_CSR_PAIRS to use it.
 #ifndef LNL_PAIR_MIN_N
+#if defined(LNL_CSR_PAIRS)
 #define LNL_PAIR_MIN_N 16384
+#else
+#define LNL_PAIR_MIN_N 0xFFFFFFFFu
+#endif
 #endif
 // CSR batches: the pair kernel (crc32c_pair.hip) after its bucket pre-pass;
 // pairs with very long datagrams go to the batch kernel (device-side count).
@@ -163,9 +171,11 @@ int launch_csr_pairs(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t 
         q.out = a.out;
         q.fold = S.fold;
         q.desc = p.desc;
-        q.nwb = p.ctl;
+        q.ctl = p.ctl;
         const uint32_t waves_max = (a.n / 2u + 1u) / 64u + 1u + lnl::kPairKeys;
-        e = lnl::launch_crc32c_pair(q, grid_for_waves(S, waves_max), st);
+        const uint32_t per_wg = lnl::kPairThreads / 64;
+        const int grid = (int)std::max(1u, std::min((waves_max + per_wg - 1) / per_wg, (uint32_t)S.cus));
+        e = lnl::launch_crc32c_pair(q, grid, st);
         if (e != hipSuccess) rc = hip_fail(e, "pair kernel launch");
     }
     if (rc == 0) {

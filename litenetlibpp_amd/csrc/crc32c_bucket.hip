@@ -26,7 +26,7 @@ namespace lnl {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kPerThread = 4;                     // count pass: many small blocks
+constexpr int kPerThread = 16;                    // count pass
 constexpr uint32_t kPerBlock = kThreads * kPerThread;
 constexpr int kScatterPerThread = 16;             // scatter pass: fewer blocks, fewer global atomics
 constexpr uint32_t kScatterPerBlock = kThreads * kScatterPerThread;
@@ -153,47 +153,48 @@ __global__ __launch_bounds__(kThreads) void pair_count_kernel(PairPrepArgs a) {
     }
 }
 
-// One workgroup: group starts (each key's count rounded up to 64; parallel
-// scan), the wave-batch count, and the padding entries.
-__global__ __launch_bounds__(kThreads) void pair_bases_kernel(PairPrepArgs a) {
+// Scatter.  Every workgroup first derives the group starts itself (each
+// key's count rounded up to 64, exclusive scan over the 512 keys in LDS);
+// workgroup 0 also writes the padding entries (idle lanes carrying the
+// group's key), the wave-batch count and the buffer's last line.
+__global__ __launch_bounds__(kThreads) void pair_scatter_kernel(PairPrepArgs a) {
     static_assert(kPairKeys == 2 * kThreads, "two keys per thread");
-    __shared__ uint32_t cnt[kPairKeys], part[kThreads];
+    constexpr uint32_t kBins = kPairKeys + 1u;
+    __shared__ uint32_t hist[kBins], base[kBins], gstart[kPairKeys], part[kThreads];
     const uint32_t t = threadIdx.x;
-    const uint32_t c0 = a.counts[2 * t], c1 = a.counts[2 * t + 1];
-    cnt[2 * t] = c0;
-    cnt[2 * t + 1] = c1;
-    const uint32_t p0 = (c0 + 63u) & ~63u, p1 = (c1 + 63u) & ~63u;
-    part[t] = p0 + p1;
-    __syncthreads();
-    // Hillis-Steele inclusive scan of the per-thread sums
-    for (uint32_t d = 1; d < kThreads; d <<= 1) {
-        const uint32_t v = t >= d ? part[t - d] : 0u;
+    for (uint32_t k = t; k < kBins; k += kThreads) hist[k] = 0;
+    {
+        const uint32_t c0 = a.counts[2 * t], c1 = a.counts[2 * t + 1];
+        const uint32_t p0 = (c0 + 63u) & ~63u, p1 = (c1 + 63u) & ~63u;
+        part[t] = p0 + p1;
         __syncthreads();
-        part[t] += v;
+        for (uint32_t d = 1; d < kThreads; d <<= 1) {  // Hillis-Steele inclusive scan
+            const uint32_t v = t >= d ? part[t - d] : 0u;
+            __syncthreads();
+            part[t] += v;
+            __syncthreads();
+        }
+        const uint32_t excl = part[t] - (p0 + p1);
+        gstart[2 * t] = excl;
+        gstart[2 * t + 1] = excl + p0;
+        if (blockIdx.x == 0) {
+            if (t == kThreads - 1) a.ctl[0] = part[t] / 64u;
+            if (t == 0) {  // last line of the buffer (the pair kernel clamps its fetches to it)
+                const uint64_t bytes = a.off[a.n] - a.off0;
+                const uint64_t b = (uint64_t)(uintptr_t)a.base;
+                a.ctl[3] = bytes ? (uint32_t)(((b + bytes - 1u) >> 7) - (b >> 7)) : 0u;
+            }
+        }
         __syncthreads();
-    }
-    const uint32_t excl = part[t] - (p0 + p1);
-    a.bases[2 * t] = excl;
-    a.bases[2 * t + 1] = excl + p0;
-    if (t == kThreads - 1) a.ctl[0] = part[t] / 64u;
-    // padding: entries count_k .. round64(count_k) of every group are idle
-    // lanes (datagram index n) carrying the group's key
-    for (uint32_t idx = t; idx < kPairKeys * 64u; idx += kThreads) {
-        const uint32_t k = idx >> 6, p = idx & 63u;
-        const uint32_t c = cnt[k];
-        if (p >= (c & 63u) && (c & 63u) != 0u) {
-            const uint32_t base = (k & 1u) ? part[k >> 1] - ((cnt[k] + 63u) & ~63u)
-                                           : part[k >> 1] - ((cnt[k] + 63u) & ~63u) - ((cnt[k + 1] + 63u) & ~63u);
-            a.desc[base + (c & ~63u) + p] = make_uint4(0u, 0u, a.n, k << 8);
+        if (blockIdx.x == 0) {
+            for (uint32_t idx = t; idx < kPairKeys * 64u; idx += kThreads) {
+                const uint32_t k = idx >> 6, p = idx & 63u;
+                const uint32_t c = a.counts[k];
+                if ((c & 63u) != 0u && p >= (c & 63u))
+                    a.desc[gstart[k] + (c & ~63u) + p] = make_uint4(0u, 0u, a.n, k << 8);
+            }
         }
     }
-}
-
-__global__ __launch_bounds__(kThreads) void pair_scatter_kernel(PairPrepArgs a) {
-    constexpr uint32_t kBins = kPairKeys + 1u;
-    __shared__ uint32_t hist[kBins], base[kBins];
-    for (uint32_t k = threadIdx.x; k < kBins; k += kThreads) hist[k] = 0;
-    __syncthreads();
     const uint32_t items = (a.n + 1u) / 2u;
     const uint32_t j0 = blockIdx.x * kScatterPerBlock + threadIdx.x;
     uint32_t key[kScatterPerThread], rank[kScatterPerThread];
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(kThreads) void pair_scatter_kernel(PairPrepArgs a) 
     for (uint32_t k = threadIdx.x; k < kBins; k += kThreads) {
         const uint32_t h = hist[k];
         if (k < kPairKeys)
-            base[k] = a.bases[k] + (h ? atomicAdd(&a.fill[k], h) : 0u);
+            base[k] = gstart[k] + (h ? atomicAdd(&a.fill[k], h) : 0u);
         else if (h)  // overflow items: 2 datagram slots each in ovf
             base[k] = atomicAdd(&a.ctl[2], h), atomicAdd(&a.ctl[1], 2u * h);
     }
@@ -242,7 +243,7 @@ void pair_prep_layout(PairPrepArgs& a, uint32_t* w) {
     const size_t items = ((size_t)a.n + 1) / 2;
     a.counts = w;
     a.fill = a.counts + (kPairKeys + 1);
-    a.ctl = a.fill + kPairKeys;  // 4 words: [0] wave-batches, [1] ovf entries, [2] ovf items
+    a.ctl = a.fill + kPairKeys;  // 4 words: [0] wave-batches, [1] ovf entries, [2] ovf items, [3] last line
     a.bases = a.ctl + 4;
     uint32_t* d = a.bases + kPairKeys;
     d += (4 - ((uintptr_t)d / 4) % 4) % 4;  // 16-byte alignment
@@ -256,7 +257,6 @@ hipError_t launch_pair_prep(const PairPrepArgs& a, hipStream_t stream) {
     if (e != hipSuccess) return e;
     const uint32_t items = (a.n + 1u) / 2u;
     hipLaunchKernelGGL(pair_count_kernel, dim3((items + kPerBlock - 1) / kPerBlock), dim3(kThreads), 0, stream, a);
-    hipLaunchKernelGGL(pair_bases_kernel, dim3(1), dim3(kThreads), 0, stream, a);
     hipLaunchKernelGGL(pair_scatter_kernel, dim3((items + kScatterPerBlock - 1) / kScatterPerBlock),
                        dim3(kThreads), 0, stream, a);
     return hipGetLastError();

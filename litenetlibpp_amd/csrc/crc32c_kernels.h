@@ -101,9 +101,10 @@ struct PairArgs {
     uint32_t* out;
     const uint32_t* fold;
     const uint4* desc;
-    const uint32_t* nwb;  // device: wave-batches
+    const uint32_t* ctl;  // device, from the pre-pass: [0] wave-batches, [3] last line of the buffer
 };
 
+constexpr int kPairThreads = 512;  // one workgroup (8 waves) per CU
 hipError_t launch_crc32c_pair(const PairArgs& a, int grid, hipStream_t stream);
 
 // Verify epilogue (crc32c_verify.hip): ok / body CRC from wire-datagram CRCs.

@@ -42,9 +42,15 @@ namespace {
 
 using namespace dev;
 
-constexpr int kWaves = kBlockThreads / 64;
-constexpr int kZeroU4 = kWaves * 2 * kBufU4 + kFoldU4;  // one zero piece after the tables
+// One 512-thread workgroup per CU (8 waves): the tables are staged once per CU,
+// which leaves room for each wave's 1 KiB descriptor slot.
+constexpr int kThreads = kPairThreads;
+constexpr int kWaves = kThreads / 64;
+constexpr int kFoldOffU4 = kWaves * 2 * kBufU4;
+constexpr int kDescOffU4 = kFoldOffU4 + kFoldU4;      // 64 descriptors per wave
+constexpr int kZeroU4 = kDescOffU4 + kWaves * 64;     // one zero piece
 constexpr int kLdsU4 = kZeroU4 + 1;
+static_assert(kLdsU4 * 16 <= 160 * 1024, "LDS");
 
 // A batch: wave-uniform schedule + this lane's descriptor (PairArgs).
 struct Pair {
@@ -53,6 +59,7 @@ struct Pair {
     uint32_t shared;  // a's last line is b's first
     uint32_t steps;   // Ta + Tb: the shared line is read at two consecutive steps
     uint4 d;          // x: run's first line, y: pad_a | be_a | pad_b | be_b, z: a, w: hasb | key
+    uint32_t lline[8];  // run's first line of lane q = 8i + lane/8 (glds instruction i)
 };
 
 __device__ LNL_INLINE uint32_t byte_of(uint32_t v, int k) { return (v >> (8 * k)) & 0xFFu; }
@@ -68,27 +75,29 @@ __device__ LNL_INLINE void make_pair(const uint4& d, uint32_t valid, Pair& P) {
     P.steps = valid ? P.Ta + P.Tb : 0u;
     P.d = d;
     if (!valid) P.d.z = 0xFFFFFFFFu;
-}
-
-// Line index of row 0 of the run of lane q = 8i + lane/8 (glds instruction i).
-__device__ LNL_INLINE void load_lines(const Pair& P, uint32_t* lline) {
     const uint32_t sub = __lane_id() >> 3;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) lline[i] = (uint32_t)__shfl((int)P.d.x, 8 * i + (int)sub, 64);
+    for (int i = 0; i < 8; ++i) P.lline[i] = (uint32_t)__shfl((int)d.x, 8 * i + (int)sub, 64);
 }
+
 
 __device__ LNL_INLINE uint4 load_desc(const PairArgs& A, uint32_t wb, uint32_t nwb) {
     return wb < nwb ? A.desc[wb * 64u + __lane_id()] : make_uint4(0u, 0u, 0xFFFFFFFFu, 0u);
 }
 
-// The descriptor of a later batch, loaded WITHOUT a compiler-inserted wait:
-// the asm load is issued before a step's row prefetch, so the next step's
-// counted `s_waitcnt vmcnt(8)` (or any vmcnt(0)) covers it -- vector memory
-// loads return in order.  make_pair reads it only after such a wait.
-__device__ LNL_INLINE void load_desc_async(const PairArgs& A, uint32_t wb, uint32_t nwb, u32x4& d) {
-    const uint32_t idx = wb < nwb ? wb * 64u + __lane_id() : 0u;
-    const uint64_t addr = (uint64_t)(uintptr_t)(A.desc + idx);
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(addr) : "memory");
+// The descriptors of a later batch go HBM -> the wave's LDS slot by LDS-DMA,
+// issued before a step's row prefetch, so the next step's counted
+// `s_waitcnt vmcnt(8)` (or any vmcnt(0)) covers them like a row; they are read
+// back (asm ds_read) at the batch change.  No compiler-visible register is
+// written asynchronously.
+__device__ LNL_INLINE void load_desc_lds(const PairArgs& A, uint32_t wb, uint32_t nwb, uint4* slot) {
+    const uint32_t idx = wb < nwb ? wb * 64u + __lane_id() : __lane_id();  // any readable entry
+    __builtin_amdgcn_global_load_lds((const void*)(A.desc + idx), (void*)slot, 16, 0, 0);
+}
+
+__device__ LNL_INLINE uint4 read_desc_lds(uint32_t slot_addr) {
+    const u32x4 v = lds_read_piece(slot_addr + 16u * __lane_id());
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 // The 8 LDS-DMA instructions of step u (64 lanes' lines) into buf.  Whole
@@ -96,18 +105,15 @@ __device__ LNL_INLINE void load_desc_async(const PairArgs& A, uint32_t wb, uint3
 // time).  Piece of glds i for this lane: slot ^ swz(8i + sub) = pc0 for even
 // i, pc0 ^ 4 for odd i.  The shared line is read at steps Ta-1 and Ta; both
 // fetches use the default cache policy so the second is served by L2.
-__device__ LNL_INLINE void issue_pair_step(const Pair& P, uint64_t base_line, uint32_t pc0, uint32_t u,
-                                           uint4* buf) {
-    // lane q's run line, fetched per step with ds_bpermute rather than held in
-    // 8 registers across the loop (register pressure is the limit here)
-    uint32_t lline[8];
-    load_lines(P, lline);
+__device__ LNL_INLINE void issue_pair_step(const Pair& P, uint64_t base_line, uint32_t max_line, uint32_t pc0,
+                                           uint32_t u, uint4* buf) {
     const uint32_t line = u - (P.shared && u >= P.Ta ? 1u : 0u);
-    const uint64_t rowbase = (base_line + line) << 7;
     const bool dflt = P.shared && (u + 1u == P.Ta || u == P.Ta);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint64_t src = rowbase + ((uint64_t)lline[i] << 7) + 16u * (pc0 ^ (4u * (i & 1)));
+        // a run never leaves the buffer; the clamp only guards the fetch
+        const uint32_t ln = min(P.lline[i] + line, max_line);
+        const uint64_t src = ((base_line + ln) << 7) + 16u * (pc0 ^ (4u * (i & 1)));
         if (dflt)
             __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (void*)(buf + 64 * i), 16, 0,
                                              LNL_PAIR_EDGE_AUX);
@@ -142,19 +148,22 @@ __device__ LNL_INLINE void read_row_framed(uint32_t rowb, uint32_t sw, uint32_t 
     read_row<0>(ad, x);
 }
 
-__global__ __launch_bounds__(kBlockThreads, 2) void crc32c_pair_kernel(PairArgs A) {
+__global__ __launch_bounds__(kThreads, 1) void crc32c_pair_kernel(PairArgs A) {
     __shared__ __attribute__((aligned(16))) uint4 lds[kLdsU4];
     const uint32_t lane = __lane_id();
     const uint32_t wave = uni(threadIdx.x >> 6);
     uint4* const buf_base = lds + wave * (2 * kBufU4);
-    uint4* const fold_lds = lds + kWaves * 2 * kBufU4;
+    uint4* const fold_lds = lds + kFoldOffU4;
+    uint4* const desc_slot = lds + kDescOffU4 + wave * 64;
+    const uint32_t desc_addr = (uint32_t)(uintptr_t)desc_slot;
     const uint32_t fold_base = (uint32_t)(uintptr_t)fold_lds;
     const uint32_t zero_addr = (uint32_t)(uintptr_t)(lds + kZeroU4);
-    const uint32_t nwb = uni(*A.nwb);
+    const uint32_t nwb = uni(A.ctl[0]);
+    const uint32_t max_line = uni(A.ctl[3]);
     if (blockIdx.x * kWaves >= nwb) return;  // whole workgroup idle (before the barrier)
     {
         const uint4* g = reinterpret_cast<const uint4*>(A.fold);
-        for (int i = threadIdx.x; i < kFoldU4; i += kBlockThreads) fold_lds[i] = g[i];
+        for (int i = threadIdx.x; i < kFoldU4; i += kThreads) fold_lds[i] = g[i];
         if (threadIdx.x == 0) lds[kZeroU4] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
     }
@@ -171,8 +180,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_pair_kernel(PairArgs 
     uint32_t wb = gw;
     make_pair(load_desc(A, wb, nwb), 1u, cur);
     make_pair(load_desc(A, wb + nw, nwb), uni(wb + nw < nwb ? 1u : 0u), nxt);
-    u32x4 raw;  // descriptor of the batch after nxt, loaded at step 0 of each batch
-    uint32_t raw_step = 0;
+    uint32_t raw_step = 0;  // step at which the slot's load (batch after nxt) was issued
 
     // step pipeline as in the batch kernel: step s lives in buffer s & 1,
     // issued two steps ahead (into the next batch near the end of this one)
@@ -183,13 +191,13 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_pair_kernel(PairArgs 
 #pragma unroll
     for (int k = 0; k < 16; ++k) Pf[k] = 0;
     if (cur.steps > 0) {
-        issue_pair_step(cur, base_line, pc0, 0, buf_base);
+        issue_pair_step(cur, base_line, max_line, pc0, 0, buf_base);
         have0 = 1;
         if (cur.steps > 1) {
-            issue_pair_step(cur, base_line, pc0, 1, buf_base + kBufU4);
+            issue_pair_step(cur, base_line, max_line, pc0, 1, buf_base + kBufU4);
             have1 = 1;
         } else if (nxt.valid && nxt.steps > 0) {
-            issue_pair_step(nxt, base_line, pc0, 0, buf_base + kBufU4);
+            issue_pair_step(nxt, base_line, max_line, pc0, 0, buf_base + kBufU4);
             have1 = 1;
         }
     }
@@ -214,7 +222,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_pair_kernel(PairArgs 
         uint4* const buf = buf_base + odd * kBufU4;
         const uint32_t rowb = row0 + odd * kBufBytes;
         if (!have0) {
-            issue_pair_step(cur, base_line, pc0, u, buf);
+            issue_pair_step(cur, base_line, max_line, pc0, u, buf);
             have1 = 0;
         }
         if (have1)
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_pair_kernel(PairArgs 
             read_row<0>(ad, x);
         }
         if (u == 0u) {
-            load_desc_async(A, wb + 2u * nw, nwb, raw);
+            load_desc_lds(A, wb + 2u * nw, nwb, desc_slot);
             raw_step = step;
         }
         // prefetch step+2 into the buffer just drained
@@ -247,10 +255,10 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_pair_kernel(PairArgs 
         {
             const uint32_t u2 = u + 2u;
             if (u2 < cur.steps) {
-                issue_pair_step(cur, base_line, pc0, u2, buf);
+                issue_pair_step(cur, base_line, max_line, pc0, u2, buf);
                 have2 = 1;
             } else if (nxt.valid && u2 - cur.steps < nxt.steps) {
-                issue_pair_step(nxt, base_line, pc0, u2 - cur.steps, buf);
+                issue_pair_step(nxt, base_line, max_line, pc0, u2 - cur.steps, buf);
                 have2 = 1;
             }
         }
@@ -302,10 +310,10 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_pair_kernel(PairArgs 
             wb += nw;
             cur = nxt;
             if (!cur.valid) break;
-            // raw was loaded at this batch's step 0; a later step's counted
-            // wait covers it unless the batch had a single step
+            // the slot was loaded at this batch's step 0; a later step's
+            // counted wait covers it unless the batch had a single step
             if (step - raw_step < 2u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            make_pair(uint4{raw.x, raw.y, raw.z, raw.w}, uni(wb + nw < nwb ? 1u : 0u), nxt);
+            make_pair(read_desc_lds(desc_addr), uni(wb + nw < nwb ? 1u : 0u), nxt);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_pair_kernel(PairArgs 
 }  // namespace
 
 hipError_t launch_crc32c_pair(const PairArgs& a, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL(crc32c_pair_kernel, dim3(grid), dim3(kBlockThreads), 0, stream, a);
+    hipLaunchKernelGGL(crc32c_pair_kernel, dim3(grid), dim3(kThreads), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -194,6 +194,20 @@ def test_csr_pairs(P, case):
     assert bad.size == 0, f"{case}: {bad.size} mismatches, first at {bad[:5]}"
 
 
+def test_csr_pairs_many_batches_per_wave(P):
+    """Far more pair batches than resident waves (persistent waves change
+    batch many times: descriptor slots, next-batch prefetch), small data."""
+    rng = np.random.default_rng(404)
+    n = 1_200_000
+    lens = rng.integers(0, 40, n)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = rng.integers(0, 256, int(off[-1]) + 1, dtype=np.uint8)
+    exp = oracle.batch_csr(data, off)
+    got = u32(P.batch_csr(dev(data), dev(off.view(np.int64), torch.int64)))
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+
+
 def test_verify_mode_bucketed(P):
     rng = np.random.default_rng(22)
     n = 30000

@@ -25,8 +25,10 @@ VARIANTS = {
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
     "k16": "-DLNL_RUN_K=16",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
-    "nobucket": "-DLNL_BUCKET_MIN_N=0xFFFFFFFFu -DLNL_PAIR_MIN_N=0xFFFFFFFFu",  # CSR: plain batch kernel
-    "nopair": "-DLNL_PAIR_MIN_N=0xFFFFFFFFu",       # CSR: bucketed batch kernel instead of the pair kernel
+    "nobucket": "-DLNL_BUCKET_MIN_N=0xFFFFFFFFu",   # CSR: plain batch kernel, no line-count pre-pass
+    "pairs": "-DLNL_CSR_PAIRS",                      # CSR / verify: the pair kernel (experiment)
+    "pair_edge_nt": "-DLNL_CSR_PAIRS -DLNL_PAIR_EDGE_AUX=2",  # pair kernel: nt for the shared-line fetches too
+    "pair_dflt": "-DLNL_CSR_PAIRS -DLNL_PAIR_AUX=0",          # pair kernel: default policy for every fetch
     "run_sc0": "-DLNL_RUN_AUX=1",
     "run_sc0nt": "-DLNL_RUN_AUX=3",
     "run_sc1": "-DLNL_RUN_AUX=16",
