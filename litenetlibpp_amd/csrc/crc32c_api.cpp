@@ -20,6 +20,7 @@
 #include "../../include/lnl_crc32c.h"
 #include "crc32c_bitslice.h"
 #include "crc32c_kernels.h"
+#include "crc32c_seg.h"
 
 namespace {
 
@@ -48,6 +49,7 @@ struct DeviceState {
     std::string init_err;
     uint8_t* dummy = nullptr;  // 256 zero bytes of device memory
     uint32_t* fold = nullptr;  // kernel tables (lnl_build_tables), 12.5 KiB
+    uint32_t* pow = nullptr;   // segment kernel's row-power tables (lnl_build_seg_tables), 3.5 KiB
     int cus = 0;
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)
@@ -83,12 +85,18 @@ int device_state(int dev, DeviceState** out) {
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(dev);
         static uint32_t host_fold[LNL_TABLE_WORDS];
+        static uint32_t host_pow[lnl::kSegPowTables * 128];
         static std::once_flag fold_once;
-        std::call_once(fold_once, [] { lnl_build_tables(host_fold); });
+        std::call_once(fold_once, [] {
+            lnl_build_tables(host_fold);
+            lnl_build_seg_tables(host_pow, (int)lnl::kSegPowTables);
+        });
         e = hipMalloc(&S.dummy, 256);
         if (e == hipSuccess) e = hipMemset(S.dummy, 0, 256);
         if (e == hipSuccess) e = hipMalloc(&S.fold, sizeof host_fold);
         if (e == hipSuccess) e = hipMemcpy(S.fold, host_fold, sizeof host_fold, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc(&S.pow, sizeof host_pow);
+        if (e == hipSuccess) e = hipMemcpy(S.pow, host_pow, sizeof host_pow, hipMemcpyHostToDevice);
         (void)hipSetDevice(cur);
         if (e != hipSuccess) {
             S.init_rc = -ENOMEM;
@@ -189,7 +197,48 @@ int launch_csr_pairs(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t 
     return rc;
 }
 
+// CSR batches of >= LNL_SEG_MIN_N datagrams: the segment kernel
+// (crc32c_seg.hip: every line read once) after its pre-pass, then the batch
+// kernel over the datagrams it leaves (device-side count).  The bucketed batch
+// kernel stays available with -DLNL_CSR_BUCKETS (experiment builds).
+#ifndef LNL_SEG_MIN_N
+#if defined(LNL_CSR_BUCKETS) || defined(LNL_CSR_PAIRS)
+#define LNL_SEG_MIN_N 0xFFFFFFFFu
+#else
+#define LNL_SEG_MIN_N 16384
+#endif
+#endif
+int launch_csr_seg(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
+    lnl::SegArgs g{};
+    g.base = a.base;
+    g.off = a.off;
+    g.off0 = a.off0;
+    g.n = a.n;
+    g.waves = (uint32_t)S.cus * (uint32_t)(lnl::kSegThreads / 64);
+    g.out = a.out;
+    g.fold = S.fold;
+    g.pow = S.pow;
+    void* scratch = nullptr;
+    const size_t bytes = lnl::seg_scratch_words(a.n, g.waves) * sizeof(uint32_t);
+    hipError_t e = hipMallocAsync(&scratch, bytes, st);
+    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
+    lnl::seg_scratch_layout(g, (uint32_t*)scratch);
+    int rc = 0;
+    e = lnl::launch_seg(g, S.cus, st);
+    if (e != hipSuccess) rc = hip_fail(e, "segment kernel launch");
+    if (rc == 0) {
+        lnl::BatchArgs o = a;
+        o.perm = g.ovf;
+        o.perm_n = g.ctl + 1;
+        rc = launch(S, o, lnl::kModeCsr, st);
+    }
+    e = hipFreeAsync(scratch, st);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
+}
+
 int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
+    if (mode == lnl::kModeCsr && a.n >= LNL_SEG_MIN_N) return launch_csr_seg(S, a, st);
     if (mode == lnl::kModeCsr && a.n >= LNL_PAIR_MIN_N) return launch_csr_pairs(S, a, st);
     if (a.n < LNL_BUCKET_MIN_N) return launch(S, a, mode, st);
     void* scratch = nullptr;
@@ -313,16 +362,16 @@ extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* 
     a.out = d_crc;
     a.ok = d_ok;
     hipStream_t st = (hipStream_t)hip_stream;
-    if (n < LNL_PAIR_MIN_N) return launch_csr(*S, a, lnl::kModeVerify, st);
-    // large batches: CRCs of the whole wire datagrams with the pair kernel,
-    // then ok / body CRC per datagram (crc32c_verify.hip)
+    if (n < LNL_SEG_MIN_N && n < LNL_PAIR_MIN_N) return launch_csr(*S, a, lnl::kModeVerify, st);
+    // large batches: CRCs of the whole wire datagrams with the segment (or
+    // pair) kernel, then ok / body CRC per datagram (crc32c_verify.hip)
     void* wire = nullptr;
     hipError_t e = hipMallocAsync(&wire, (size_t)n * 4u, st);
     if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync: %s", hipGetErrorString(e));
     lnl::BatchArgs w = a;
     w.out = (uint32_t*)wire;
     w.ok = nullptr;
-    int rc = launch_csr_pairs(*S, w, st);
+    int rc = n >= LNL_SEG_MIN_N ? launch_csr_seg(*S, w, st) : launch_csr_pairs(*S, w, st);
     if (rc == 0) {
         lnl::VerifyArgs v{};
         v.base = d_base;

@@ -107,6 +107,53 @@ LNL_HD inline void lnl_build_tables(uint32_t* t) {
     for (int pad = 0; pad < 128; ++pad) t[LNL_TABLE_C_OFF + pad] = lnl_step_bits(0xFFFFFFFFu, -8 * pad);
 }
 
+// Inverse of a 32x32 GF(2) matrix given by its columns (Gauss-Jordan).
+LNL_HD inline void lnl_cols_inverse(const uint32_t* cols, uint32_t* inv) {
+    uint32_t row[32], aug[32];
+    for (int i = 0; i < 32; ++i) {
+        uint32_t r = 0;
+        for (int k = 0; k < 32; ++k) r |= ((cols[k] >> i) & 1u) << k;
+        row[i] = r;
+        aug[i] = 1u << i;
+    }
+    for (int c = 0; c < 32; ++c) {
+        int p = c;
+        while (!((row[p] >> c) & 1u)) ++p;
+        const uint32_t tr = row[p], ta = aug[p];
+        row[p] = row[c];
+        aug[p] = aug[c];
+        row[c] = tr;
+        aug[c] = ta;
+        for (int i = 0; i < 32; ++i)
+            if (i != c && ((row[i] >> c) & 1u)) {
+                row[i] ^= row[c];
+                aug[i] ^= aug[c];
+            }
+    }
+    for (int k = 0; k < 32; ++k) {
+        uint32_t v = 0;
+        for (int i = 0; i < 32; ++i) v |= ((aug[i] >> k) & 1u) << i;
+        inv[k] = v;
+    }
+}
+
+// Row-power tables of the segment kernel (crc32c_seg.hip): table b is A^(2^b),
+// A = L^-1 step^1024 L -- one 128-byte row in the basis lnl_fold_tree's result
+// lives in -- as 8 nibble tables (128 words).  A fold result r of a prefix that
+// is followed by m more rows becomes A^m r.
+LNL_HD inline void lnl_build_seg_tables(uint32_t* t, int ntables) {
+    uint32_t L[32], Li[32], A[32], A2[32];
+    for (int k = 0; k < 32; ++k) L[k] = lnl_step_bits(LNL_CRC32C_POLY, 992 - 32 * k);
+    lnl_cols_inverse(L, Li);
+    for (int k = 0; k < 32; ++k) A[k] = lnl_cols_apply(Li, lnl_step_bits(L[k], 1024));
+    for (int b = 0; b < ntables; ++b) {
+        for (int k = 0; k < 8; ++k)
+            for (uint32_t v = 0; v < 16; ++v) t[b * 128 + k * 16 + v] = lnl_cols_apply(A, v << (4 * k));
+        for (int k = 0; k < 32; ++k) A2[k] = lnl_cols_apply(A, A[k]);
+        for (int k = 0; k < 32; ++k) A[k] = A2[k];
+    }
+}
+
 LNL_HD LNL_INLINE uint32_t lnl_table_b(uint32_t e) { return e & 15u; }
 LNL_HD LNL_INLINE uint32_t lnl_table_a(uint32_t e) { return 16u + (e >> 4); }
 

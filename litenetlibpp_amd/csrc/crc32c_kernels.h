@@ -107,6 +107,32 @@ struct PairArgs {
 constexpr int kPairThreads = 512;  // one workgroup (8 waves) per CU
 hipError_t launch_crc32c_pair(const PairArgs& a, int grid, hipStream_t stream);
 
+// CSR segment kernel (crc32c_seg.hip): every line of the batch read once, lane
+// g owns the datagrams ending in segment g (crc32c_seg.h).  launch_seg enqueues
+// the counter reset, the pre-pass, the kernel and the cross-wave fix-up; the
+// caller then runs the batch kernel over ovf (perm_n = ctl + 1).
+constexpr int kSegThreads = 512;  // one workgroup (8 waves) per CU
+struct SegArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    uint64_t off0;
+    uint32_t n;
+    uint32_t waves;         // resident waves of the kernel's grid (CUs x 8)
+    uint32_t* out;
+    const uint32_t* fold;   // LNL_TABLE_WORDS words (lnl_build_tables)
+    const uint32_t* pow;    // kSegPowTables x 128 words (lnl_build_seg_tables)
+    uint32_t* ctl;          // 4 words: [1] overflow datagrams
+    uint32_t* first;        // seg_max_segments(waves) + 1
+    uint32_t* ovf;          // n: datagrams left to the batch kernel
+    uint32_t* carry;        // seg_max_segments(waves) / 64: each wave-batch's lane-63 tail
+    uint4* fix;             // same count: each wave-batch's lane-0 head
+};
+
+hipError_t launch_seg(const SegArgs& a, int grid, hipStream_t stream);
+// scratch words (u32) launch_seg needs for n datagrams on `waves` resident waves
+size_t seg_scratch_words(uint32_t n, uint32_t waves);
+void seg_scratch_layout(SegArgs& a, uint32_t* scratch);
+
 // Verify epilogue (crc32c_verify.hip): ok / body CRC from wire-datagram CRCs.
 struct VerifyArgs {
     const uint8_t* base;

@@ -55,3 +55,21 @@ def test_kernel_lane_emulation(tmp_path):
     r = subprocess.run([str(exe), "1500"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bad=0" in r.stdout
+
+
+def test_segment_kernel_emulation(tmp_path):
+    """tests/emu/emu_seg.cpp: the CSR segment kernel's whole launch (pre-pass,
+    per-lane row events, head/tail combine, cross-wave fix-up, overflow list)
+    on the CPU, every datagram written exactly once with the oracle's CRC:
+    mixed 64..1400 B, tiny (segments with more ends than a lane tracks),
+    datagrams over many segments, lengths on line and segment boundaries,
+    empty datagrams, several wave counts and buffer offsets."""
+    oracle.load()
+    exe = tmp_path / "emu_seg"
+    src = os.path.join(ROOT, "tests", "emu", "emu_seg.cpp")
+    so_dir = os.path.dirname(oracle.ORACLE_SO)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src, f"-L{so_dir}",
+                    "-lcrc32c_oracle", f"-Wl,-rpath,{so_dir}"], check=True)
+    r = subprocess.run([str(exe), "0.2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bad=0" in r.stdout

@@ -194,6 +194,48 @@ def test_csr_pairs(P, case):
     assert bad.size == 0, f"{case}: {bad.size} mismatches, first at {bad[:5]}"
 
 
+@pytest.mark.parametrize("case", ["segment_multiples", "line_multiples", "lead_and_tail", "tiny_excess"])
+def test_csr_segments(P, case):
+    """CSR segment kernel (crc32c_seg.hip, the default for >= 16 Ki datagrams):
+    datagram ends on segment boundaries (lengths of 2 KiB multiples, the
+    segment size of batches this small), on line boundaries, a batch that
+    starts and ends mid-line, and segments with more ends than a lane tracks
+    (left to the batch kernel)."""
+    rng = np.random.default_rng(["segment_multiples", "line_multiples", "lead_and_tail", "tiny_excess"].index(case) + 500)
+    n = 40000
+    if case == "segment_multiples":
+        lens = 2048 * rng.integers(1, 4, n) - rng.choice([0, 0, 1], n)
+    elif case == "line_multiples":
+        lens = 128 * rng.integers(0, 13, n)
+    elif case == "tiny_excess":
+        lens = np.where(rng.random(n) < 0.7, rng.integers(0, 20, n), rng.integers(20, 1433, n))
+    else:
+        lens = rng.integers(0, 1433, n)
+    lead = 0 if case == "segment_multiples" else int(rng.integers(1, 128))
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(lead)
+    data = rng.integers(0, 256, int(off[-1]) + 77, dtype=np.uint8)
+    exp = oracle.batch_csr(data, off)
+    got = u32(P.batch_csr(dev(data), dev(off.view(np.int64), torch.int64)))
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{case}: {bad.size} mismatches, first at {bad[:5]}"
+
+
+def test_csr_segments_several_batches_per_wave(P):
+    """A batch larger than one segment per lane at the largest segment size
+    (> 2 GiB on 256 CUs): waves take several wave-batches."""
+    rng = np.random.default_rng(600)
+    n = 1_700_000
+    lens = rng.integers(1200, 1433, n)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(601)
+    d = torch.randint(0, 256, (int(off[-1]),), dtype=torch.uint8, device="cuda", generator=g)
+    got = u32(P.batch_csr(d, dev(off.view(np.int64), torch.int64)))
+    exp = oracle.batch_csr(d.cpu().numpy(), off)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+
+
 def test_csr_pairs_many_batches_per_wave(P):
     """Far more pair batches than resident waves (persistent waves change
     batch many times: descriptor slots, next-batch prefetch), small data."""
