@@ -199,13 +199,15 @@ int launch_csr_pairs(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t 
 
 // CSR batches of >= LNL_SEG_MIN_N datagrams: the segment kernel
 // (crc32c_seg.hip: every line read once) after its pre-pass, then the batch
-// kernel over the datagrams it leaves (device-side count).  The bucketed batch
-// kernel stays available with -DLNL_CSR_BUCKETS (experiment builds).
+// kernel over the datagrams it leaves (device-side count).  An experiment, off
+// by default: it is VALU-bound (datagram ends fall on different rows in each
+// lane, so nearly every row pays a divergent fold) and measured 0.30 ms against
+// 0.18 ms for the bucketed batch kernel on config 3.  Build with -DLNL_CSR_SEG.
 #ifndef LNL_SEG_MIN_N
-#if defined(LNL_CSR_BUCKETS) || defined(LNL_CSR_PAIRS)
-#define LNL_SEG_MIN_N 0xFFFFFFFFu
-#else
+#if defined(LNL_CSR_SEG)
 #define LNL_SEG_MIN_N 16384
+#else
+#define LNL_SEG_MIN_N 0xFFFFFFFFu
 #endif
 #endif
 int launch_csr_seg(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {

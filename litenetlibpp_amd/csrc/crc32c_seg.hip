@@ -176,6 +176,16 @@ __device__ LNL_INLINE uint32_t init_word(uint32_t fold_base, uint32_t pad) {
     return lds_read_u32(fold_base + 4u * (LNL_TABLE_C_OFF + pad));  // C[pad]
 }
 
+// The fold at a datagram end.  Diagnostic build only (-DLNL_SEG_DIAG_NOFOLD):
+// a 2-op stand-in (wrong CRCs), to measure what the folds cost.
+__device__ LNL_INLINE uint32_t seg_fold(uint32_t* s) {
+#if defined(LNL_SEG_DIAG_NOFOLD)
+    return s[0] ^ s[31];
+#else
+    return lnl_fold_tree(s);
+#endif
+}
+
 // A^m r (m < 2^kSegPowTables)
 __device__ LNL_INLINE uint32_t pow_apply(uint32_t pow_base, uint32_t m, uint32_t r) {
 #pragma unroll
@@ -377,7 +387,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_seg_kernel(SegArgs A) {
             uint32_t ini = 0u;
             if (ev0) {
                 if (track) {
-                    const uint32_t r = lnl_fold_tree(o);
+                    const uint32_t r = seg_fold(o);
                     if (head) {
                         r_head = r;
                         m_head = t + 1u;
@@ -407,7 +417,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_seg_kernel(SegArgs A) {
                         v[w] &= ~m;
                     }
                     xe[0] ^= ini;
-                    if (track) A.out[cid] = final_crc(fold_base, 127u - be2, lnl_fold_tree(xe));
+                    if (track) A.out[cid] = final_crc(fold_base, 127u - be2, seg_fold(xe));
                     advance();
                     ini = active && track && cs < (int32_t)rowend ? init_word(fold_base, (uint32_t)cs - rowst) : 0u;
                     ev = active && ce <= rowend;

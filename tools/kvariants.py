@@ -25,9 +25,10 @@ VARIANTS = {
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
     "k16": "-DLNL_RUN_K=16",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
-    "buckets": "-DLNL_CSR_BUCKETS",                 # CSR: bucketed batch kernel instead of the segment kernel
-    "seg_dflt": "-DLNL_SEG_AUX=0",                  # segment kernel: default cache policy
-    "nobucket": "-DLNL_CSR_BUCKETS -DLNL_BUCKET_MIN_N=0xFFFFFFFFu",  # CSR: plain batch kernel, no pre-pass
+    "seg": "-DLNL_CSR_SEG",                         # CSR: segment kernel instead of the bucketed batch kernel
+    "seg_dflt": "-DLNL_CSR_SEG -DLNL_SEG_AUX=0",    # segment kernel: default cache policy
+    "seg_nofold": "-DLNL_CSR_SEG -DLNL_SEG_DIAG_NOFOLD",  # segment kernel without its folds (wrong CRCs): their cost
+    "nobucket": "-DLNL_BUCKET_MIN_N=0xFFFFFFFFu",   # CSR: plain batch kernel, no pre-pass
     "pairs": "-DLNL_CSR_PAIRS",                      # CSR / verify: the pair kernel (experiment)
     "pair_edge_nt": "-DLNL_CSR_PAIRS -DLNL_PAIR_EDGE_AUX=2",  # pair kernel: nt for the shared-line fetches too
     "pair_dflt": "-DLNL_CSR_PAIRS -DLNL_PAIR_AUX=0",          # pair kernel: default policy for every fetch

@@ -20,6 +20,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "litenetlibpp_amd", "tools"))
 from prof_summary import from_db, short  # noqa: E402
 
+# kernels of liblnl_crc32c.so (rocprofv3 names contain these)
+PRODUCT_KERNELS = ("crc32c_", "bucket_count", "bucket_scatter", "pair_count", "pair_scatter",
+                   "seg_prep", "seg_fixup", "verify_from_wire")
+
 
 def main():
     tag, wl = sys.argv[1], sys.argv[2]
@@ -32,28 +36,39 @@ def main():
           f"--no-cpu-baseline`\n",
           "Produced by `tools/profile_round.sh` on one MI355X; each section is a separate rocprofv3 run "
           "(kernel trace; then one PMC pass per counter group).\n"]
-    pmc_means = {}
-    crc_kernel = None
+    # HBM bytes per API call: every product kernel the call launches (the CRC
+    # kernel plus, for CSR, its bucket pre-pass), counter totals divided by the
+    # dispatch count of the dominant CRC kernel (the one with the most time)
+    pmc_tot = {}
+    kernels = set()
+    trace_stats = None
     for part in ("trace", "fetch", "write", "clk", "sq"):
         d = os.path.join(src, part)
         db = [f for f in os.listdir(d) if f.endswith(".db")][0]
         out = subprocess.run([sys.executable, os.path.join(ROOT, "litenetlibpp_amd", "tools", "prof_summary.py"),
                               os.path.join(d, db)], capture_output=True, text=True, check=True).stdout
         md.append(f"## {part}\n\n" + out.split("\n", 2)[2])
-        _, _, pmc = from_db(os.path.join(d, db))
+        stats, _, pmc = from_db(os.path.join(d, db))
+        if part == "trace":
+            trace_stats = stats
         for name, cs in pmc.items():
-            if "crc32c" in name:
-                crc_kernel = short(name)
+            if any(k in name for k in PRODUCT_KERNELS):
+                kernels.add(short(name))
                 for cn, vals in cs.items():
-                    pmc_means[cn] = sum(vals) / len(vals)
+                    pmc_tot[cn] = pmc_tot.get(cn, 0.0) + sum(vals)
+    crc = {n: d for n, d in trace_stats.items() if "crc32c" in n}
+    dom = max(crc, key=lambda n: sum(crc[n]))
+    crc_kernel = short(dom)
+    calls = len(crc[dom])
+    pmc_means = {cn: v / calls for cn, v in pmc_tot.items()}
     with open(os.path.join(dst, f"{tag}_{wl}_summary.md"), "w") as f:
         f.write("\n".join(md))
     fetch = pmc_means["FETCH_SIZE"] * 1024 * 2
     write = pmc_means["WRITE_SIZE"] * 1024
-    tr = {"kernel": crc_kernel, "workload": wl, "hbm_bytes_per_launch": round(fetch + write),
+    tr = {"kernel": crc_kernel, "kernels_per_call": sorted(kernels), "workload": wl, "hbm_bytes_per_launch": round(fetch + write),
           "fetch_bytes": round(fetch), "write_bytes": round(write),
           "how": "rocprofv3 PMC passes (tools/profile_round.sh): FETCH_SIZE (KiB) x 1024 x 2 "
-                 "(gfx950 counts half of wide streaming reads) + WRITE_SIZE (KiB) x 1024, mean per dispatch",
+                 "(gfx950 counts half of wide streaming reads) + WRITE_SIZE (KiB) x 1024, summed over the product kernels of one API call",
           "source": f"profiles/{tag}_{wl}_summary.md"}
     with open(os.path.join(dst, f"traffic_{wl}.json"), "w") as f:
         json.dump(tr, f, indent=1)
