@@ -138,8 +138,8 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
 }
 
 // CSR / verify batches: bucket the datagrams by line count first (crc32c_bucket.hip)
-// so that every wave's lanes need the same number of rows.  The permutation
-// lives in stream-ordered scratch (hipMallocAsync / hipFreeAsync on `st`), so
+// so that every wave's lanes need the same number of rows.  The descriptors
+// live in stream-ordered scratch (hipMallocAsync / hipFreeAsync on `st`), so
 // concurrent calls on different streams never share it.  Small batches skip
 // the pre-pass (its fixed cost would dominate).
 #ifndef LNL_BUCKET_MIN_N
@@ -244,7 +244,8 @@ int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st)
     if (mode == lnl::kModeCsr && a.n >= LNL_PAIR_MIN_N) return launch_csr_pairs(S, a, st);
     if (a.n < LNL_BUCKET_MIN_N) return launch(S, a, mode, st);
     void* scratch = nullptr;
-    const size_t bytes = (2 * lnl::kBuckets + (size_t)a.n) * sizeof(uint32_t);
+    // counts + fill (kBucketCounterWords, a multiple of 16 bytes), then the descriptors
+    const size_t bytes = lnl::kBucketCounterWords * sizeof(uint32_t) + (size_t)a.n * sizeof(uint4);
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
     if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
     lnl::BucketArgs b{};
@@ -254,14 +255,14 @@ int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st)
     b.n = a.n;
     b.verify = mode == lnl::kModeVerify;
     b.counts = (uint32_t*)scratch;
-    b.fill = b.counts + lnl::kBuckets;
-    b.perm = b.fill + lnl::kBuckets;
+    b.fill = b.counts + lnl::kCounterCopies * lnl::kBuckets;
+    b.desc = (uint4*)(b.counts + lnl::kBucketCounterWords);
     e = lnl::launch_csr_buckets(b, st);
     int rc = 0;
     if (e != hipSuccess) {
         rc = hip_fail(e, "bucket pre-pass launch");
     } else {
-        a.perm = b.perm;
+        a.desc = b.desc;
         rc = launch(S, a, mode, st);
     }
     e = hipFreeAsync(scratch, st);

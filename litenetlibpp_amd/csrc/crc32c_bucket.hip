@@ -5,17 +5,25 @@
 // longest datagram touches lines.  With lengths uniform in 64..1400 B the
 // longest of 64 random datagrams almost always spans 12 lines while the mean
 // is ~6.7, so nearly half of all row slots would fetch the zero line.  This
-// pre-pass writes a permutation `perm` that lists the datagrams bucket by
-// bucket (bucket = line count, 0 for empty datagrams, kBuckets-1 for very
-// long ones); the batch kernel then takes its 64 lanes from consecutive perm
-// entries, so a wave's lanes need the same number of rows.
+// pre-pass writes one 16-byte descriptor per datagram (index, CRC length,
+// start), listed bucket by bucket (bucket = line count, 0 for empty
+// datagrams, kBuckets-1 for very long ones); the batch kernel then takes its
+// 64 lanes from consecutive descriptors -- one coalesced 16-byte load per lane
+// instead of an index plus two random offset reads -- so a wave's lanes need
+// the same number of rows.
 //
 // Two passes over the offsets (8 bytes per datagram each), both cheap next to
-// the payload: count per bucket (workgroup histogram in LDS, one global
-// atomic per workgroup and bucket), then scatter (the workgroup reserves a
-// range per bucket with one global atomic and places its datagrams with their
-// LDS ranks).  Order within a bucket depends on atomic order; CRCs are written
-// by datagram index, so results do not.
+// the payload: count per bucket (wave histograms in LDS, one global atomic
+// per workgroup and bucket), then scatter (the workgroup reserves a range per
+// bucket with one global atomic and places its datagrams with their LDS
+// ranks).  The global counters exist in kCounterCopies copies (workgroup w
+// uses copy w % kCounterCopies; each bucket's range is split into one
+// sub-range per copy), so no counter takes more than 64 of the 1024
+// workgroups' atomics -- with a single copy the serialized atomics made both
+// passes ~50 % slower.  Order within a bucket depends on atomic order; CRCs are written by
+// datagram index, so results do not.  Workgroups take 1024 datagrams each, so
+// a config-3 batch (2^20) launches 1024 of them: four per CU keep enough
+// offset loads in flight.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,17 +34,21 @@ namespace lnl {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kPerThread = 16;                    // count pass
+constexpr int kPerThread = 16;                    // pair count pass
 constexpr uint32_t kPerBlock = kThreads * kPerThread;
-constexpr int kScatterPerThread = 16;             // scatter pass: fewer blocks, fewer global atomics
+constexpr int kScatterPerThread = 16;             // pair scatter pass
 constexpr uint32_t kScatterPerBlock = kThreads * kScatterPerThread;
+constexpr int kBucketPerThread = 4;               // bucket count and scatter passes
+constexpr uint32_t kBucketPerBlock = kThreads * kBucketPerThread;
 
-__device__ inline uint32_t bucket_of(const BucketArgs& a, uint32_t i) {
+// bucket, CRC length and start (relative to base) of datagram i
+__device__ inline uint32_t bucket_of(const BucketArgs& a, uint32_t i, uint32_t& len, uint64_t& start) {
     const uint64_t s = a.off[i], e = a.off[i + 1];
     const uint32_t total = (uint32_t)(e - s);
-    const uint32_t len = a.verify ? (total >= 5u ? total - 4u : 0u) : total;
+    len = a.verify ? (total >= 5u ? total - 4u : 0u) : total;
+    start = s - a.off0;
     if (len == 0) return 0;
-    const uint64_t abs0 = (uint64_t)(uintptr_t)a.base + (s - a.off0);
+    const uint64_t abs0 = (uint64_t)(uintptr_t)a.base + start;
     const uint64_t abs1 = abs0 + len - 1u;
     const uint64_t t = (abs1 >> 7) - (abs0 >> 7) + 1u;
     return t < (uint64_t)kBuckets ? (uint32_t)t : (uint32_t)kBuckets - 1u;
@@ -48,55 +60,75 @@ __global__ __launch_bounds__(kThreads) void bucket_count_kernel(BucketArgs a) {
     __shared__ uint32_t hist[kW][kBuckets];
     for (int k = threadIdx.x; k < kW * kBuckets; k += kThreads) (&hist[0][0])[k] = 0;
     __syncthreads();
-    const uint32_t i0 = blockIdx.x * kPerBlock + threadIdx.x;
-    uint32_t key[kPerThread];
+    const uint32_t i0 = blockIdx.x * kBucketPerBlock + threadIdx.x;
+    uint32_t key[kBucketPerThread];
 #pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {  // all loads first
+    for (int j = 0; j < kBucketPerThread; ++j) {  // all loads first
         const uint32_t i = i0 + j * kThreads;
-        key[j] = i < a.n ? bucket_of(a, i) : kBuckets;
+        uint32_t len;
+        uint64_t start;
+        key[j] = i < a.n ? bucket_of(a, i, len, start) : kBuckets;
     }
     uint32_t* h = hist[threadIdx.x >> 6];
 #pragma unroll
-    for (int j = 0; j < kPerThread; ++j)
+    for (int j = 0; j < kBucketPerThread; ++j)
         if (key[j] < kBuckets) atomicAdd(&h[key[j]], 1u);
     __syncthreads();
     if (threadIdx.x < kBuckets) {
         uint32_t c = 0;
 #pragma unroll
         for (int w = 0; w < kW; ++w) c += hist[w][threadIdx.x];
-        if (c) atomicAdd(&a.counts[threadIdx.x], c);
+        if (c) atomicAdd(&a.counts[(blockIdx.x % kCounterCopies) * kBuckets + threadIdx.x], c);
     }
 }
 
 __global__ __launch_bounds__(kThreads) void bucket_scatter_kernel(BucketArgs a) {
-    __shared__ uint32_t hist[kBuckets], base[kBuckets];
-    if (threadIdx.x < kBuckets) hist[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t i0 = blockIdx.x * kScatterPerBlock + threadIdx.x;
-    uint32_t key[kScatterPerThread], rank[kScatterPerThread];
+    __shared__ uint32_t hist[kBuckets], base[kBuckets], tot[kBuckets], part[kBuckets];
+    const uint32_t copy = blockIdx.x % kCounterCopies;
+    if (threadIdx.x < kBuckets) {
+        // bucket b's range is split into kCounterCopies sub-ranges, one per
+        // counter copy: total over copies, and the copies before this one
+        uint32_t t = 0, p = 0;
 #pragma unroll
-    for (int j = 0; j < kScatterPerThread; ++j) {  // all loads first
+        for (uint32_t c = 0; c < kCounterCopies; ++c) {
+            const uint32_t v = a.counts[c * kBuckets + threadIdx.x];
+            t += v;
+            p += c < copy ? v : 0u;
+        }
+        hist[threadIdx.x] = 0;
+        tot[threadIdx.x] = t;
+        part[threadIdx.x] = p;
+    }
+    __syncthreads();
+    const uint32_t i0 = blockIdx.x * kBucketPerBlock + threadIdx.x;
+    uint32_t key[kBucketPerThread], rank[kBucketPerThread], len[kBucketPerThread];
+    uint64_t start[kBucketPerThread];
+#pragma unroll
+    for (int j = 0; j < kBucketPerThread; ++j) {  // all loads first
         const uint32_t i = i0 + j * kThreads;
-        key[j] = i < a.n ? bucket_of(a, i) : 0u;
+        key[j] = i < a.n ? bucket_of(a, i, len[j], start[j]) : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < kScatterPerThread; ++j) {
+    for (int j = 0; j < kBucketPerThread; ++j) {
         const uint32_t i = i0 + j * kThreads;
         rank[j] = i < a.n ? atomicAdd(&hist[key[j]], 1u) : 0u;
     }
     __syncthreads();
     if (threadIdx.x < kBuckets) {
-        // exclusive prefix of the global counts (64 values) + this block's range
+        // exclusive prefix of the global counts + this block's range
         uint32_t before = 0;
-        for (uint32_t k = 0; k < threadIdx.x; ++k) before += a.counts[k];
+        for (uint32_t k = 0; k < threadIdx.x; ++k) before += tot[k];
         const uint32_t h = hist[threadIdx.x];
-        base[threadIdx.x] = before + (h ? atomicAdd(&a.fill[threadIdx.x], h) : 0u);
+        base[threadIdx.x] = before + part[threadIdx.x] +
+                            (h ? atomicAdd(&a.fill[copy * kBuckets + threadIdx.x], h) : 0u);
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kScatterPerThread; ++j) {
+    for (int j = 0; j < kBucketPerThread; ++j) {
         const uint32_t i = i0 + j * kThreads;
-        if (i < a.n) a.perm[base[key[j]] + rank[j]] = i;
+        if (i < a.n)
+            a.desc[base[key[j]] + rank[j]] =
+                make_uint4(i, len[j], (uint32_t)start[j], (uint32_t)(start[j] >> 32));
     }
 }
 
@@ -263,12 +295,11 @@ hipError_t launch_pair_prep(const PairPrepArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(a.counts, 0, 2 * kBuckets * sizeof(uint32_t), stream);  // counts + fill
+    hipError_t e = hipMemsetAsync(a.counts, 0, kBucketCounterWords * sizeof(uint32_t), stream);  // counts + fill
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(bucket_count_kernel, dim3((a.n + kPerBlock - 1) / kPerBlock), dim3(kThreads), 0, stream,
-                       a);
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((a.n + kScatterPerBlock - 1) / kScatterPerBlock),
-                       dim3(kThreads), 0, stream, a);
+    const dim3 grid((a.n + kBucketPerBlock - 1) / kBucketPerBlock);
+    hipLaunchKernelGGL(bucket_count_kernel, grid, dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL(bucket_scatter_kernel, grid, dim3(kThreads), 0, stream, a);
     return hipGetLastError();
 }
 

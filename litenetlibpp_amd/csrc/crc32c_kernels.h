@@ -22,7 +22,9 @@ struct BatchArgs {
     uint8_t* ok;           // Verify mode: 1 = trailing CRC matches
     const uint8_t* dummy;  // 16 readable bytes (library scratch) for idle glds lanes
     const uint32_t* fold;  // LNL_TABLE_WORDS words from lnl_build_tables (device)
-    const uint32_t* perm;  // optional: lane datagrams perm[64 b + lane] (CSR buckets)
+    const uint32_t* perm;  // optional: lane datagrams perm[64 b + lane] (pair / segment leftovers)
+    const uint4* desc;     // optional, instead of perm + off: lane descriptors desc[64 b + lane]
+                           // {datagram, CRC length, start (lo, hi) relative to base} (CSR buckets)
     const uint32_t* perm_n;  // optional (device): number of perm entries, else n
 };
 
@@ -46,10 +48,12 @@ struct RunArgs {
 
 hipError_t launch_crc32c_run(const RunArgs& a, int grid, hipStream_t stream);
 
-// CSR pre-pass (crc32c_bucket.hip): perm[] = datagrams grouped by the number
-// of 128-byte lines they touch.  counts and fill: 2 * kBuckets words of
-// device scratch (zeroed by the launch).
+// CSR pre-pass (crc32c_bucket.hip): desc[] = descriptors of the datagrams
+// grouped by the number of 128-byte lines they touch.  counts and fill:
+// kBucketCounterWords words of device scratch (zeroed by the launch).
 constexpr int kBuckets = 64;
+constexpr uint32_t kCounterCopies = 16;  // copies of the global bucket counters (atomic contention)
+constexpr uint32_t kBucketCounterWords = 2 * kCounterCopies * kBuckets;  // counts + fill
 struct BucketArgs {
     const uint8_t* base;
     const uint64_t* off;
@@ -57,8 +61,8 @@ struct BucketArgs {
     uint32_t n;
     uint32_t verify;  // verify mode: the CRC covers all but the last 4 bytes
     uint32_t* counts;
-    uint32_t* fill;   // counts + kBuckets
-    uint32_t* perm;   // n entries
+    uint32_t* fill;   // counts + kCounterCopies * kBuckets
+    uint4* desc;      // n entries (BatchArgs::desc layout), 16-byte aligned
 };
 
 hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream);

@@ -141,12 +141,17 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
     B.valid = uni(b < nbatch ? 1u : 0u);
     uint64_t start;
     uint32_t len;
-    {
-        const uint32_t idx = b * 64u + lane;
-        const bool real = B.valid && idx < nperm;
+    const uint32_t idx = b * 64u + lane;
+    const bool real = B.valid && idx < nperm;
+    if (kMode != kModeFixed && a.desc) {  // uniform branch: bucketed CSR / verify
+        const uint4 d = real ? a.desc[idx] : make_uint4(a.n, 0u, 0u, 0u);
+        B.p = d.x;
+        len = d.y;
+        start = (uint64_t)d.z | ((uint64_t)d.w << 32);
+    } else {
         B.p = real ? (a.perm ? a.perm[idx] : idx) : a.n;
+        lane_extent<kMode>(a, B.p, start, len);
     }
-    lane_extent<kMode>(a, B.p, start, len);
     const uint64_t abs0 = (uint64_t)(uintptr_t)a.base + start;
     const uint64_t abs1 = abs0 + len - 1u;  // last byte (unused when len == 0)
     const uint32_t idle = len == 0u ? 1u : 0u;
