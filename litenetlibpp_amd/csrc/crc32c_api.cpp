@@ -12,6 +12,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <mutex>
@@ -145,17 +147,34 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
 #ifndef LNL_BUCKET_MIN_N
 #define LNL_BUCKET_MIN_N 16384
 #endif
-// The CSR pair kernel (crc32c_pair.hip) is an experiment, off by default: it
-// fetches 13 % fewer HBM bytes on config 3 than the bucketed batch kernel but
-// streams them at ~5.0 TB/s against ~6.1 TB/s, and its pre-pass is heavier
-// (0.233 vs 0.184 ms per config-3 batch).  Build with -DLNL_CSR_PAIRS to use it.
-#ifndef LNL_PAIR_MIN_N
-#if defined(LNL_CSR_PAIRS)
-#define LNL_PAIR_MIN_N 16384
-#else
-#define LNL_PAIR_MIN_N 0xFFFFFFFFu
-#endif
-#endif
+// CSR kernel selection.  The default is the bucketed batch kernel; the other
+// three are experiments kept for measurement (tools/kvariants.py) and covered
+// by the parity tests, which switch paths with lnl_crc32c_set_csr_path():
+//   uniform  crc32c_csr.hip: uniform line-count batches, shared lines fetched
+//            once (786 MB instead of 968 MB per config-3 batch) -- but its
+//            kernel streams them slower and its plan + tail epilogue cost more:
+//            0.188 vs 0.175 ms per config-3 batch
+//   seg      crc32c_seg.hip: VALU-bound (datagram ends fall on different rows
+//            in each lane, so nearly every row pays a divergent fold): 0.33 ms
+//   pairs    crc32c_pair.hip: 13 % fewer bytes, streamed at ~5.0 TB/s: 0.233 ms
+// The initial value comes from the environment (LNL_CSR_PATH=bucketed |
+// uniform | seg | pairs).
+enum CsrPath : int { kPathBucketed = 0, kPathUniform = 1, kPathSeg = 2, kPathPairs = 3 };
+std::atomic<int> g_csr_path{-1};
+int csr_path() {
+    int p = g_csr_path.load(std::memory_order_relaxed);
+    if (p >= 0) return p;
+    p = kPathBucketed;
+    if (const char* e = getenv("LNL_CSR_PATH")) {
+        if (!strcmp(e, "uniform")) p = kPathUniform;
+        else if (!strcmp(e, "seg")) p = kPathSeg;
+        else if (!strcmp(e, "pairs")) p = kPathPairs;
+    }
+    int expect = -1;
+    g_csr_path.compare_exchange_strong(expect, p);
+    return g_csr_path.load();
+}
+
 // CSR batches: the pair kernel (crc32c_pair.hip) after its bucket pre-pass;
 // pairs with very long datagrams go to the batch kernel (device-side count).
 int launch_csr_pairs(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
@@ -197,19 +216,9 @@ int launch_csr_pairs(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t 
     return rc;
 }
 
-// CSR batches of >= LNL_SEG_MIN_N datagrams: the segment kernel
-// (crc32c_seg.hip: every line read once) after its pre-pass, then the batch
-// kernel over the datagrams it leaves (device-side count).  An experiment, off
-// by default: it is VALU-bound (datagram ends fall on different rows in each
-// lane, so nearly every row pays a divergent fold) and measured 0.30 ms against
-// 0.18 ms for the bucketed batch kernel on config 3.  Build with -DLNL_CSR_SEG.
-#ifndef LNL_SEG_MIN_N
-#if defined(LNL_CSR_SEG)
-#define LNL_SEG_MIN_N 16384
-#else
-#define LNL_SEG_MIN_N 0xFFFFFFFFu
-#endif
-#endif
+// CSR batches: the segment kernel (crc32c_seg.hip: every line read once)
+// after its pre-pass, then the batch kernel over the datagrams it leaves
+// (device-side count).
 int launch_csr_seg(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
     lnl::SegArgs g{};
     g.base = a.base;
@@ -239,10 +248,58 @@ int launch_csr_seg(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st
     return rc;
 }
 
+// CSR batches: the uniform path (crc32c_csr.hip), then the batch kernel over
+// its overflow datagrams, which also XORs the shared-line tail contributions
+// into out.
+int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
+    void* scratch = nullptr;
+    const size_t bytes = lnl::csr_plan_scratch_words(a.n) * sizeof(uint32_t);
+    hipError_t e = hipMallocAsync(&scratch, bytes, st);
+    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
+    lnl::CsrPlanArgs p{};
+    p.base = a.base;
+    p.off = a.off;
+    p.off0 = a.off0;
+    p.n = a.n;
+    p.out = a.out;
+    lnl::csr_plan_layout(p, (uint32_t*)scratch);
+    lnl::CsrArgs c{};
+    c.base = a.base;
+    c.desc = p.desc;
+    c.ctl = p.ctl;
+    c.out = a.out;
+    c.tail = p.tail;
+    c.dummy = S.dummy;
+    c.fold = S.fold;
+    c.amat = S.pow;  // table 0 = A^(2^0)
+    // batches <= n / 64 + one partial batch per key
+    const uint32_t waves_max = a.n / 64u + lnl::kBuckets;
+    int rc = 0;
+    e = lnl::launch_csr_uniform(p, c, grid_for_waves(S, waves_max), st);
+    if (e != hipSuccess) rc = hip_fail(e, "CSR uniform launch");
+    if (rc == 0) {
+        lnl::BatchArgs o = a;
+        o.perm = p.ovf;
+        o.perm_n = p.ctl + 1;
+        o.tail_xor = p.tail;
+        o.xor_n = a.n;
+        rc = launch(S, o, lnl::kModeCsr, st);
+    }
+    e = hipFreeAsync(scratch, st);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
+}
+
 int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
-    if (mode == lnl::kModeCsr && a.n >= LNL_SEG_MIN_N) return launch_csr_seg(S, a, st);
-    if (mode == lnl::kModeCsr && a.n >= LNL_PAIR_MIN_N) return launch_csr_pairs(S, a, st);
     if (a.n < LNL_BUCKET_MIN_N) return launch(S, a, mode, st);
+    if (mode == lnl::kModeCsr) {
+        switch (csr_path()) {
+            case kPathUniform: return launch_csr_uniform(S, a, st);
+            case kPathSeg: return launch_csr_seg(S, a, st);
+            case kPathPairs: return launch_csr_pairs(S, a, st);
+            default: break;
+        }
+    }
     void* scratch = nullptr;
     // counts + fill (kBucketCounterWords, a multiple of 16 bytes), then the descriptors
     const size_t bytes = lnl::kBucketCounterWords * sizeof(uint32_t) + (size_t)a.n * sizeof(uint4);
@@ -305,6 +362,16 @@ extern "C" const char* lnl_crc32c_last_error(void) { return g_err.c_str(); }
 
 extern "C" int lnl_crc32c_abi_version(void) { return LNL_CRC32C_ABI_VERSION; }
 
+// Experiment knob, not part of include/lnl_crc32c.h: selects the kernel of
+// large CSR / verify batches (0 bucketed batch kernel, 1 uniform, 2 segment,
+// 3 pair; see csr_path above).  Returns the previous path, or -EINVAL.
+extern "C" int lnl_crc32c_set_csr_path(int path) {
+    if (path < kPathBucketed || path > kPathPairs) return fail(-EINVAL, "CSR path %d out of range", path);
+    const int prev = csr_path();
+    g_csr_path.store(path);
+    return prev;
+}
+
 extern "C" int lnl_crc32c_batch_fixed_dev(const uint8_t* d_base, size_t stride, uint32_t len,
                                           uint32_t n, uint32_t* d_out, void* hip_stream) {
     if (n == 0) return 0;
@@ -365,16 +432,19 @@ extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* 
     a.out = d_crc;
     a.ok = d_ok;
     hipStream_t st = (hipStream_t)hip_stream;
-    if (n < LNL_SEG_MIN_N && n < LNL_PAIR_MIN_N) return launch_csr(*S, a, lnl::kModeVerify, st);
-    // large batches: CRCs of the whole wire datagrams with the segment (or
-    // pair) kernel, then ok / body CRC per datagram (crc32c_verify.hip)
+    const int path = csr_path();
+    if (n < LNL_BUCKET_MIN_N || path == kPathBucketed) return launch_csr(*S, a, lnl::kModeVerify, st);
+    // large batches on an experiment path: CRCs of the whole wire datagrams
+    // with that path's kernel, then ok / body CRC per datagram (crc32c_verify.hip)
     void* wire = nullptr;
     hipError_t e = hipMallocAsync(&wire, (size_t)n * 4u, st);
     if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync: %s", hipGetErrorString(e));
     lnl::BatchArgs w = a;
     w.out = (uint32_t*)wire;
     w.ok = nullptr;
-    int rc = n >= LNL_SEG_MIN_N ? launch_csr_seg(*S, w, st) : launch_csr_pairs(*S, w, st);
+    int rc = path == kPathSeg ? launch_csr_seg(*S, w, st)
+             : path == kPathPairs ? launch_csr_pairs(*S, w, st)
+                                  : launch_csr_uniform(*S, w, st);
     if (rc == 0) {
         lnl::VerifyArgs v{};
         v.base = d_base;

@@ -26,6 +26,8 @@ struct BatchArgs {
     const uint4* desc;     // optional, instead of perm + off: lane descriptors desc[64 b + lane]
                            // {datagram, CRC length, start (lo, hi) relative to base} (CSR buckets)
     const uint32_t* perm_n;  // optional (device): number of perm entries, else n
+    const uint32_t* tail_xor;  // optional: out[i] ^= tail_xor[i] for all i < n first (CSR uniform path)
+    uint32_t xor_n;            // entries of tail_xor
 };
 
 // Enqueue one batch kernel on `stream` with `grid` workgroups.
@@ -136,6 +138,39 @@ hipError_t launch_seg(const SegArgs& a, int grid, hipStream_t stream);
 // scratch words (u32) launch_seg needs for n datagrams on `waves` resident waves
 size_t seg_scratch_words(uint32_t n, uint32_t waves);
 void seg_scratch_layout(SegArgs& a, uint32_t* scratch);
+
+// CSR uniform path (crc32c_csr.hip): plan pre-pass + uniform line-count
+// batches that fetch each shared boundary line once.  The caller then runs
+// the batch kernel over ovf (perm_n = ctl + 1) with tail_xor = tail.
+constexpr uint32_t kCsrMaxRows = 63;  // longer datagrams (> 8 KiB) go to the batch kernel
+constexpr uint64_t kCsrMaxLine = (1u << 25) - 64u;  // and those starting >= ~4 GiB after base
+struct CsrPlanArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    uint64_t off0;
+    uint32_t n;
+    uint32_t* out;     // CRC 0 for empty datagrams
+    uint32_t* counts;  // kBucketCounterWords (counts + fill), then ctl
+    uint32_t* fill;
+    uint32_t* ctl;     // [0] uniform batches, [1] overflow datagrams
+    uint4* desc;       // n + 64 * kBuckets entries
+    uint32_t* tail;    // n: tail contribution of datagram i (0 unless it drops its last line)
+    uint32_t* ovf;     // n: overflow datagrams
+};
+struct CsrArgs {
+    const uint8_t* base;
+    const uint4* desc;
+    const uint32_t* ctl;
+    uint32_t* out;
+    uint32_t* tail;
+    const uint8_t* dummy;
+    const uint32_t* fold;  // LNL_TABLE_WORDS (lnl_build_tables)
+    const uint32_t* amat;  // 128 words: A as nibble tables (lnl_build_seg_tables, table 0)
+};
+size_t csr_plan_scratch_words(uint32_t n);
+void csr_plan_layout(CsrPlanArgs& a, uint32_t* scratch);
+// zeroes the counters, then plan count / plan scatter / uniform kernel
+hipError_t launch_csr_uniform(const CsrPlanArgs& p, const CsrArgs& c, int grid, hipStream_t stream);
 
 // Verify epilogue (crc32c_verify.hip): ok / body CRC from wire-datagram CRCs.
 struct VerifyArgs {

@@ -256,6 +256,14 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
     uint4* const fold_lds = lds + kWaves * 2 * kBufU4;
     const uint32_t fold_base = (uint32_t)(uintptr_t)fold_lds;
 
+    // CSR uniform path epilogue: fold the tail contributions into out (a
+    // datagram this launch computes itself has tail 0 and is not touched)
+    if (a.tail_xor) {
+        for (uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x; i < a.xor_n; i += gridDim.x * kBlockThreads) {
+            const uint32_t v = a.tail_xor[i];
+            if (v) a.out[i] ^= v;
+        }
+    }
     // entries to process: n, or a device-side count of perm entries
     const uint32_t nperm = a.perm_n ? uni(*a.perm_n) : a.n;
     const uint32_t nbatch = (nperm + 63u) >> 6;

@@ -31,6 +31,22 @@ def P():
     return pkg
 
 
+# Large CSR / verify batches (>= 16 Ki datagrams) have four kernel paths in the
+# library (crc32c_api.cpp, csr_path): the default bucketed batch kernel and three
+# experiments.  The large-batch tests run on every path.
+CSR_PATHS = {"bucketed": 0, "uniform": 1, "seg": 2, "pairs": 3}
+all_paths = pytest.mark.parametrize("csr_path", list(CSR_PATHS), indirect=True)
+
+
+@pytest.fixture
+def csr_path(P, request):
+    L = P.lib()
+    prev = L.lnl_crc32c_set_csr_path(CSR_PATHS[request.param])
+    assert prev >= 0
+    yield request.param
+    L.lnl_crc32c_set_csr_path(prev)
+
+
 def u32(t):
     return t.cpu().numpy().view(np.uint32)
 
@@ -148,7 +164,8 @@ def test_csr_mixed_length_config3_shape(P):
     assert np.array_equal(got, exp)
 
 
-def test_csr_bucketed_mix(P):
+@all_paths
+def test_csr_bucketed_mix(P, csr_path):
     """Batches large enough for the line-count bucketing pre-pass
     (crc32c_bucket.hip): empty, 1..3-byte, line-crossing and very long
     datagrams (line-count bucket 63) mixed, buffer not line-aligned."""
@@ -169,7 +186,8 @@ def test_csr_bucketed_mix(P):
 
 
 @pytest.mark.parametrize("case", ["odd_n", "tiny", "line_multiples", "overflow_heavy"])
-def test_csr_pairs(P, case):
+@all_paths
+def test_csr_pairs(P, csr_path, case):
     """CSR pair kernel (crc32c_pair.hip): a lone last datagram (odd n), pairs of
     tiny datagrams sharing one line, lengths that end exactly on line
     boundaries (unshared pairs), and many pairs too long for the pair buckets
@@ -195,9 +213,9 @@ def test_csr_pairs(P, case):
 
 
 @pytest.mark.parametrize("case", ["segment_multiples", "line_multiples", "lead_and_tail", "tiny_excess"])
-def test_csr_segments(P, case):
-    """CSR segment kernel (crc32c_seg.hip, the default for >= 16 Ki datagrams):
-    datagram ends on segment boundaries (lengths of 2 KiB multiples, the
+@all_paths
+def test_csr_segments(P, csr_path, case):
+    """Shapes aimed at the CSR segment kernel (crc32c_seg.hip): datagram ends on segment boundaries (lengths of 2 KiB multiples, the
     segment size of batches this small), on line boundaries, a batch that
     starts and ends mid-line, and segments with more ends than a lane tracks
     (left to the batch kernel)."""
@@ -220,7 +238,8 @@ def test_csr_segments(P, case):
     assert bad.size == 0, f"{case}: {bad.size} mismatches, first at {bad[:5]}"
 
 
-def test_csr_segments_several_batches_per_wave(P):
+@all_paths
+def test_csr_segments_several_batches_per_wave(P, csr_path):
     """A batch larger than one segment per lane at the largest segment size
     (> 2 GiB on 256 CUs): waves take several wave-batches."""
     rng = np.random.default_rng(600)
@@ -236,7 +255,8 @@ def test_csr_segments_several_batches_per_wave(P):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
 
 
-def test_csr_pairs_many_batches_per_wave(P):
+@all_paths
+def test_csr_pairs_many_batches_per_wave(P, csr_path):
     """Far more pair batches than resident waves (persistent waves change
     batch many times: descriptor slots, next-batch prefetch), small data."""
     rng = np.random.default_rng(404)
@@ -250,7 +270,8 @@ def test_csr_pairs_many_batches_per_wave(P):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
 
 
-def test_verify_mode_bucketed(P):
+@all_paths
+def test_verify_mode_bucketed(P, csr_path):
     rng = np.random.default_rng(22)
     n = 30000
     lens = rng.integers(0, 1433, n)
@@ -283,7 +304,8 @@ def test_verify_mode_bucketed(P):
     assert np.array_equal(u32(crc)[big], want_crc[big])
 
 
-def test_full_config3_bit_exact(P):
+@all_paths
+def test_full_config3_bit_exact(P, csr_path):
     # BASELINE config 3 at full size: 2^20 datagrams of 64..1400 B, CSR
     rng = np.random.default_rng(43)
     lens = 64 + rng.integers(0, 1337, 1 << 20)

@@ -25,13 +25,16 @@ VARIANTS = {
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
     "k16": "-DLNL_RUN_K=16",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
-    "seg": "-DLNL_CSR_SEG",                         # CSR: segment kernel instead of the bucketed batch kernel
-    "seg_dflt": "-DLNL_CSR_SEG -DLNL_SEG_AUX=0",    # segment kernel: default cache policy
-    "seg_nofold": "-DLNL_CSR_SEG -DLNL_SEG_DIAG_NOFOLD",  # segment kernel without its folds (wrong CRCs): their cost
+    # CSR experiment paths: same library, runtime path (lnl_crc32c_set_csr_path)
+    "uniform": ("", 1),                             # CSR: uniform line-count batches, shared lines once
+    "seg": ("", 2),                                 # CSR: segment kernel
+    "pairs": ("", 3),                               # CSR: pair kernel
+    "seg_nofold": ("-DLNL_SEG_DIAG_NOFOLD", 2),     # segment kernel without its folds (wrong CRCs): their cost
     "nobucket": "-DLNL_BUCKET_MIN_N=0xFFFFFFFFu",   # CSR: plain batch kernel, no pre-pass
-    "pairs": "-DLNL_CSR_PAIRS",                      # CSR / verify: the pair kernel (experiment)
-    "pair_edge_nt": "-DLNL_CSR_PAIRS -DLNL_PAIR_EDGE_AUX=2",  # pair kernel: nt for the shared-line fetches too
-    "pair_dflt": "-DLNL_CSR_PAIRS -DLNL_PAIR_AUX=0",          # pair kernel: default policy for every fetch
+    "csr_edge_nt": ("-DLNL_CSR_EDGE_AUX=2", 1),     # uniform kernel: nt for rows 0 / R-1 too
+    "csr_dflt": ("-DLNL_CSR_AUX=0", 1),             # uniform kernel: default policy for the middle rows
+    "pair_edge_nt": ("-DLNL_PAIR_EDGE_AUX=2", 3),   # pair kernel: nt for the shared-line fetches too
+    "pair_dflt": ("-DLNL_PAIR_AUX=0", 3),           # pair kernel: default policy for every fetch
     "run_sc0": "-DLNL_RUN_AUX=1",
     "run_sc0nt": "-DLNL_RUN_AUX=3",
     "run_sc1": "-DLNL_RUN_AUX=16",
@@ -45,10 +48,15 @@ VARIANTS = {
 }
 
 
+def flags_path(v):
+    """VARIANTS entry -> (extra -D flags, CSR path or None)."""
+    return (v, None) if isinstance(v, str) else v
+
+
 def build(names):
     for n in names:
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "litenetlibpp_amd"), "variant",
-                        f"NAME={n}", f"VFLAGS={VARIANTS[n]}"], check=True)
+                        f"NAME={n}", f"VFLAGS={flags_path(VARIANTS[n])[0]}"], check=True)
         print("built", n)
 
 
@@ -62,6 +70,9 @@ def run(names, rounds, workloads):
                                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         L.lnl_crc32c_batch_csr_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                ctypes.c_void_p, ctypes.c_void_p]
+        path = flags_path(VARIANTS[n])[1]
+        if path is not None:
+            L.lnl_crc32c_set_csr_path(path)
         libs[n] = L
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
