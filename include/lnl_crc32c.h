@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 1
+#define LNL_CRC32C_ABI_VERSION 2
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -105,6 +105,17 @@ int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint
  * PCIe rate; pageable ones work but copy through a staging buffer. */
 int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                           uint32_t* h_out, int device);
+
+/* Multi-device form of lnl_crc32c_batch_host: the batch
+ * is split into ndev contiguous datagram ranges of ceil(n / ndev) (the last
+ * possibly shorter or empty), range r runs on devices[r] through
+ * lnl_crc32c_batch_host on its own host thread, all ranges concurrently; no
+ * data crosses between devices.  Blocks until every range is done.  A device
+ * may appear more than once (its ranges then run one after the other).
+ * Returns 0, or the first failing range's code (message via
+ * lnl_crc32c_last_error on the calling thread). */
+int lnl_crc32c_batch_host_multi(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
+                                uint32_t* h_out, const int* devices, int ndev);
 
 /* ---- misc ---------------------------------------------------------------- */
 

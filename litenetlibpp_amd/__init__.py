@@ -11,6 +11,7 @@ from .crc32c import (  # noqa: F401
     batch_csr,
     batch_fixed,
     batch_host,
+    batch_host_multi,
     crc32c,
     crc32c_extend,
     mtu_with_layer,

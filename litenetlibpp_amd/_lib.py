@@ -56,6 +56,8 @@ def lib() -> ctypes.CDLL:
                                             ctypes.c_void_p]
     L.lnl_crc32c_batch_host.restype = ctypes.c_int
     L.lnl_crc32c_batch_host.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, ctypes.c_int]
+    L.lnl_crc32c_batch_host_multi.restype = ctypes.c_int
+    L.lnl_crc32c_batch_host_multi.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, ctypes.c_int]
     L.lnl_crc32c_last_error.restype = ctypes.c_char_p
     L.lnl_crc32c_last_error.argtypes = []
     L.lnl_crc32c_abi_version.restype = ctypes.c_int

@@ -32,7 +32,7 @@ HEADER_SIZE = 1        # net_constants::HEADER_SIZE (/root/reference/include/lnl
 
 __all__ = [
     "Crc32cError", "EXTRA_PACKET_SIZE", "crc32c", "crc32c_extend", "Crc32cLayer",
-    "batch_fixed", "batch_csr", "verify_csr", "batch_host", "mtu_with_layer",
+    "batch_fixed", "batch_csr", "verify_csr", "batch_host", "batch_host_multi", "mtu_with_layer",
 ]
 
 
@@ -191,4 +191,22 @@ def batch_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.nda
     if n > 0:
         check(lib().lnl_crc32c_batch_host(data.ctypes.data, offsets.ctypes.data, n, out.ctypes.data,
                                           device), "lnl_crc32c_batch_host")
+    return out
+
+
+def batch_host_multi(data: np.ndarray, offsets: np.ndarray, devices) -> np.ndarray:
+    """Host-resident batch split over several GPUs (contiguous datagram ranges
+    of ceil(n / len(devices)), one host thread per range, no data exchanged
+    between devices).  Blocking.  Mirrors lnl_crc32c_batch_host_multi."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets).astype(np.uint64, copy=False)
+    devs = np.ascontiguousarray(list(devices), dtype=np.int32)
+    if devs.size == 0:
+        raise ValueError("empty device list")
+    n = offsets.size - 1
+    out = np.empty(max(n, 0), dtype=np.uint32)
+    if n > 0:
+        check(lib().lnl_crc32c_batch_host_multi(data.ctypes.data, offsets.ctypes.data, n, out.ctypes.data,
+                                                devs.ctypes.data, int(devs.size)),
+              "lnl_crc32c_batch_host_multi")
     return out

@@ -18,6 +18,8 @@
 #include <cstdio>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/lnl_crc32c.h"
 #include "crc32c_bitslice.h"
@@ -99,6 +101,18 @@ int device_state(int dev, DeviceState** out) {
         if (e == hipSuccess) e = hipMemcpy(S.fold, host_fold, sizeof host_fold, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&S.pow, sizeof host_pow);
         if (e == hipSuccess) e = hipMemcpy(S.pow, host_pow, sizeof host_pow, hipMemcpyHostToDevice);
+        // CSR / verify calls take their scratch from the stream-ordered pool
+        // (hipMallocAsync / hipFreeAsync on the caller's stream).  Keep freed
+        // blocks in the pool across synchronisations: with the default
+        // threshold (0) the pool trims at every sync and the next call's
+        // hipMallocAsync goes back to the driver.
+        if (e == hipSuccess) {
+            hipMemPool_t pool = nullptr;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
+                uint64_t keep = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+            }
+        }
         (void)hipSetDevice(cur);
         if (e != hipSuccess) {
             S.init_rc = -ENOMEM;
@@ -553,5 +567,31 @@ extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_of
     }
     for (int s = 0; s < 2; ++s)
         if ((e = hipStreamSynchronize(S->streams[s])) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return 0;
+}
+
+extern "C" int lnl_crc32c_batch_host_multi(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
+                                           uint32_t* h_out, const int* devices, int ndev) {
+    if (n == 0) return 0;
+    if (!devices || ndev <= 0) return fail(-EINVAL, "empty device list");
+    if (!h_base || !h_off || !h_out) return fail(-EINVAL, "NULL argument");
+    const uint32_t per = (uint32_t)(((uint64_t)n + (uint64_t)ndev - 1) / (uint64_t)ndev);
+    std::vector<int> rc(ndev, 0);
+    std::vector<std::string> err(ndev);
+    std::vector<std::thread> th;
+    th.reserve(ndev);
+    for (int r = 0; r < ndev; ++r) {
+        const uint32_t start = (uint32_t)std::min<uint64_t>((uint64_t)r * per, n);
+        const uint32_t cnt = std::min(per, n - start);
+        if (cnt == 0) continue;
+        th.emplace_back([&, r, start, cnt] {
+            // the range's offsets stay absolute (h_off[start] may be nonzero)
+            rc[r] = lnl_crc32c_batch_host(h_base, h_off + start, cnt, h_out + start, devices[r]);
+            if (rc[r]) err[r] = g_err;  // thread_local: copy before the thread ends
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int r = 0; r < ndev; ++r)
+        if (rc[r]) return fail(rc[r], "range %d (device %d): %s", r, devices[r], err[r].c_str());
     return 0;
 }

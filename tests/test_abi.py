@@ -34,7 +34,8 @@ def test_header_declares_the_boundary():
     syms = declared_symbols()
     for s in ("lnl_crc32c", "lnl_crc32c_extend", "lnl_crc32c_batch_fixed_dev",
               "lnl_crc32c_batch_csr_dev", "lnl_crc32c_batch_host", "lnl_crc32c_verify_csr_dev",
-              "lnl_crc32c_layer_outbound", "lnl_crc32c_layer_inbound", "lnl_crc32c_last_error"):
+              "lnl_crc32c_layer_outbound", "lnl_crc32c_layer_inbound", "lnl_crc32c_last_error",
+              "lnl_crc32c_batch_host_multi"):
         assert s in syms
 
 
@@ -44,7 +45,7 @@ def test_library_exports_every_declared_symbol(pkg):
     exported = set(re.findall(r"\bT (lnl_\w+)", out))
     missing = [s for s in declared_symbols() if s not in exported]
     assert not missing, missing
-    assert pkg.lib().lnl_crc32c_abi_version() == 1
+    assert pkg.lib().lnl_crc32c_abi_version() == 2
 
 
 def test_cpu_crc_matches_oracle(pkg):
@@ -97,3 +98,13 @@ def test_batch_entry_points_refuse_without_gpu(pkg):
     assert list(out) == [0, 0, 0, 0]
     # n == 0 is valid and touches nothing
     assert L.lnl_crc32c_batch_fixed_dev(None, 0, 0, 0, None, None) == 0
+    # the multi-device host form: every range fails the same way, nothing computed
+    off = (ctypes.c_uint64 * 5)(0, 16, 32, 48, 64)
+    devs = (ctypes.c_int * 2)(0, 0)
+    rc = L.lnl_crc32c_batch_host_multi(ctypes.addressof(buf), ctypes.addressof(off), 4, ctypes.addressof(out),
+                                       ctypes.addressof(devs), 2)
+    assert rc == -19, rc
+    assert b"range" in L.lnl_crc32c_last_error()
+    assert list(out) == [0, 0, 0, 0]
+    assert L.lnl_crc32c_batch_host_multi(ctypes.addressof(buf), ctypes.addressof(off), 4, ctypes.addressof(out),
+                                         None, 0) == -22

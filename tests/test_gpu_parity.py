@@ -410,6 +410,21 @@ def test_host_streaming_path(P):
     assert np.array_equal(P.batch_host(pinned.numpy(), off, 0), exp)
 
 
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_host_multi_device_path(P, devices):
+    """lnl_crc32c_batch_host_multi: contiguous ranges of ceil(n / ndev), one
+    host thread each (one GPU on the test box: the same device listed several
+    times), nonzero first offset, n not a multiple of ndev."""
+    rng = np.random.default_rng(31 + len(devices))
+    n = 70001
+    lens = rng.integers(0, 1433, n)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(13)
+    data = rng.integers(0, 256, int(off[-1]) + 5, dtype=np.uint8)
+    pinned = torch.from_numpy(data).pin_memory().numpy()
+    got = P.batch_host_multi(pinned, off, devices)
+    assert np.array_equal(got, oracle.batch_csr(data, off))
+
+
 def test_full_config2_bit_exact(P):
     # BASELINE config 2 at full size: 2^20 x 1400 B, every CRC compared
     n, L = 1 << 20, 1400
