@@ -397,6 +397,13 @@ __global__ __launch_bounds__(kThreads, 2) void crc32c_csr_kernel(CsrArgs a) {
             have1 = have2;
         }
         const bool last = t + 1u == cur.R;
+#if defined(LNL_CSR_DIAG_MEMONLY)  // diagnostic build: rows loaded and read, no framing / network / fold
+#pragma unroll
+        for (int k = 0; k < 32; ++k) s[k] = (t == 0u ? 0u : s[k]) ^ x[k];
+        ++step;
+        if (last) {
+            if (!f_idle(cur.fr)) a.out[cur.p] = s[0] ^ s[31];
+#else
         if (last) {  // the datagram's end (lanes that keep their last line)
 #pragma unroll
             for (int w = 0; w < 32; ++w) x[w] &= f_drop(cur.fr) ? 0xFFFFFFFFu : below_mask(w, f_be(cur.fr) + 1u);
@@ -441,6 +448,7 @@ __global__ __launch_bounds__(kThreads, 2) void crc32c_csr_kernel(CsrArgs a) {
             r = f_drop(cur.fr) ? ra : r;
             r = final_map(fold_base, 127u - f_be(cur.fr), r);
             if (!f_idle(cur.fr)) a.out[cur.p] = ~r;
+#endif
             t = 0;
             b += nw;
             cur = nxt;

@@ -33,6 +33,7 @@ VARIANTS = {
     "nobucket": "-DLNL_BUCKET_MIN_N=0xFFFFFFFFu",   # CSR: plain batch kernel, no pre-pass
     "csr_edge_nt": ("-DLNL_CSR_EDGE_AUX=2", 1),     # uniform kernel: nt for rows 0 / R-1 too
     "csr_dflt": ("-DLNL_CSR_AUX=0", 1),             # uniform kernel: default policy for the middle rows
+    "csr_memonly": ("-DLNL_CSR_DIAG_MEMONLY", 1),   # uniform kernel, rows loaded and read only (wrong CRCs)
     "pair_edge_nt": ("-DLNL_PAIR_EDGE_AUX=2", 3),   # pair kernel: nt for the shared-line fetches too
     "pair_dflt": ("-DLNL_PAIR_AUX=0", 3),           # pair kernel: default policy for every fetch
     "run_sc0": "-DLNL_RUN_AUX=1",
