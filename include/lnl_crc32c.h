@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 2
+#define LNL_CRC32C_ABI_VERSION 3
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -80,6 +80,22 @@ int64_t lnl_crc32c_layer_outbound(const uint8_t* data, size_t offset, size_t len
  * looks like packet loss to the reliability layer). */
 int64_t lnl_crc32c_layer_inbound(const uint8_t* data, size_t length);
 
+/* net_packet::verify() (/root/reference/include/lnl/net_packet.h:120-131) of a
+ * packet data[0..size) after the layer has stripped its CRC: 1 if the property
+ * (data[0] & 0x1F) is a known one and size covers its header (plus the 6-byte
+ * fragment header when data[0] & 0x80), else 0.  size 0 gives 0. */
+int lnl_packet_verify(const uint8_t* data, size_t size);
+
+/* The whole inbound acceptance test of one wire datagram, as net_manager would
+ * apply it with the layer on (receive_logic :218-222, then
+ * on_message_received :343): LNL_INBOUND_DROP_CRC (length < 5 or CRC
+ * mismatch), LNL_INBOUND_MALFORMED (CRC fine, verify() fails) or
+ * LNL_INBOUND_ACCEPT (strip 4 bytes and dispatch). */
+#define LNL_INBOUND_DROP_CRC 0
+#define LNL_INBOUND_ACCEPT 1
+#define LNL_INBOUND_MALFORMED 2
+int lnl_inbound_status(const uint8_t* data, size_t length);
+
 /* ---- batched GPU path (gfx950 kernels) ----------------------------------- */
 
 /* out[i] = CRC32C(d_base + i*stride, len), i < n.  stride >= len. */
@@ -97,6 +113,12 @@ int lnl_crc32c_batch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint3
  * NULL) receives the CRC computed over the first length-4 bytes. */
 int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
                               uint8_t* d_ok, uint32_t* d_crc, void* hip_stream);
+
+/* Batched inbound filter: lnl_inbound_status of every
+ * datagram of a CSR batch of wire datagrams, in one pass -- d_status[i] is
+ * LNL_INBOUND_DROP_CRC, LNL_INBOUND_ACCEPT or LNL_INBOUND_MALFORMED. */
+int lnl_inbound_filter_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                               uint8_t* d_status, void* hip_stream);
 
 /* Host-resident batch (the socket path): copies h_base/h_off to `device`
  * in chunks over two HIP streams (H2D -> kernel -> D2H overlapped), writes

@@ -12,6 +12,12 @@ from .crc32c import (  # noqa: F401
     batch_fixed,
     batch_host,
     batch_host_multi,
+    inbound_filter,
+    inbound_status,
+    packet_verify,
+    INBOUND_ACCEPT,
+    INBOUND_DROP_CRC,
+    INBOUND_MALFORMED,
     crc32c,
     crc32c_extend,
     mtu_with_layer,

@@ -58,6 +58,12 @@ def lib() -> ctypes.CDLL:
     L.lnl_crc32c_batch_host.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, ctypes.c_int]
     L.lnl_crc32c_batch_host_multi.restype = ctypes.c_int
     L.lnl_crc32c_batch_host_multi.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, ctypes.c_int]
+    L.lnl_packet_verify.restype = ctypes.c_int
+    L.lnl_packet_verify.argtypes = [_c_u8p, ctypes.c_size_t]
+    L.lnl_inbound_status.restype = ctypes.c_int
+    L.lnl_inbound_status.argtypes = [_c_u8p, ctypes.c_size_t]
+    L.lnl_inbound_filter_csr_dev.restype = ctypes.c_int
+    L.lnl_inbound_filter_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, ctypes.c_void_p]
     L.lnl_crc32c_last_error.restype = ctypes.c_char_p
     L.lnl_crc32c_last_error.argtypes = []
     L.lnl_crc32c_abi_version.restype = ctypes.c_int

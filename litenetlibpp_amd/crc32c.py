@@ -33,6 +33,8 @@ HEADER_SIZE = 1        # net_constants::HEADER_SIZE (/root/reference/include/lnl
 __all__ = [
     "Crc32cError", "EXTRA_PACKET_SIZE", "crc32c", "crc32c_extend", "Crc32cLayer",
     "batch_fixed", "batch_csr", "verify_csr", "batch_host", "batch_host_multi", "mtu_with_layer",
+    "packet_verify", "inbound_status", "inbound_filter",
+    "INBOUND_DROP_CRC", "INBOUND_ACCEPT", "INBOUND_MALFORMED",
 ]
 
 
@@ -179,6 +181,36 @@ def verify_csr(data, offsets, want_crc: bool = False, stream=None):
                                               crc.data_ptr() if crc is not None else None,
                                               _stream_handle(stream)), "lnl_crc32c_verify_csr_dev")
     return (ok, crc) if want_crc else ok
+
+
+INBOUND_DROP_CRC, INBOUND_ACCEPT, INBOUND_MALFORMED = 0, 1, 2  # include/lnl_crc32c.h
+
+
+def packet_verify(packet) -> bool:
+    """net_packet::verify() of a packet (CRC already stripped), on the CPU."""
+    addr, n, _keep = _addr(packet)
+    return bool(lib().lnl_packet_verify(addr, n))
+
+
+def inbound_status(wire) -> int:
+    """INBOUND_DROP_CRC / INBOUND_ACCEPT / INBOUND_MALFORMED for one wire
+    datagram (layer check, then verify() of the stripped packet), on the CPU."""
+    addr, n, _keep = _addr(wire)
+    return int(lib().lnl_inbound_status(addr, n))
+
+
+def inbound_filter(data, offsets, stream=None):
+    """Batched inbound filter on the GPU: status[i] of every wire datagram of a
+    CSR batch (uint8: INBOUND_DROP_CRC / INBOUND_ACCEPT / INBOUND_MALFORMED)."""
+    torch = _torch()
+    _check_dev_u8(data, "data")
+    _check_off(offsets, data)
+    n = offsets.numel() - 1
+    status = torch.empty(max(n, 0), dtype=torch.uint8, device=data.device)
+    if n > 0:
+        check(lib().lnl_inbound_filter_csr_dev(data.data_ptr(), offsets.data_ptr(), n, status.data_ptr(),
+                                               _stream_handle(stream)), "lnl_inbound_filter_csr_dev")
+    return status
 
 
 def batch_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:

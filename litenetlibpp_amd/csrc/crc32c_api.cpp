@@ -432,8 +432,24 @@ extern "C" int lnl_crc32c_batch_csr_dev(const uint8_t* d_base, const uint64_t* d
     return launch_csr(*S, a, lnl::kModeCsr, (hipStream_t)hip_stream);
 }
 
+namespace {
+int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t* d_ok, uint32_t* d_crc,
+               uint32_t filter, void* hip_stream);
+}  // namespace
+
 extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
                                          uint8_t* d_ok, uint32_t* d_crc, void* hip_stream) {
+    return verify_csr(d_base, d_off, n, d_ok, d_crc, 0u, hip_stream);
+}
+
+extern "C" int lnl_inbound_filter_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                          uint8_t* d_status, void* hip_stream) {
+    return verify_csr(d_base, d_off, n, d_status, nullptr, 1u, hip_stream);
+}
+
+namespace {
+int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t* d_ok, uint32_t* d_crc,
+               uint32_t filter, void* hip_stream) {
     if (n == 0) return 0;
     if (!d_ok || !d_off) return fail(-EINVAL, "d_ok / d_off is NULL");
     if (!d_base) return fail(-EINVAL, "d_base is NULL");
@@ -445,6 +461,7 @@ extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* 
     a.n = n;
     a.out = d_crc;
     a.ok = d_ok;
+    a.filter = filter;
     hipStream_t st = (hipStream_t)hip_stream;
     const int path = csr_path();
     if (n < LNL_BUCKET_MIN_N || path == kPathBucketed) return launch_csr(*S, a, lnl::kModeVerify, st);
@@ -467,6 +484,7 @@ extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* 
         v.wire = (const uint32_t*)wire;
         v.ok = d_ok;
         v.crc = d_crc;
+        v.filter = filter;
         e = lnl::launch_verify_from_wire(v, st);
         if (e != hipSuccess) rc = hip_fail(e, "verify epilogue launch");
     }
@@ -474,6 +492,7 @@ extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* 
     if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
     return rc;
 }
+}  // namespace
 
 // Host-resident batch: chunks of whole datagrams alternate over two streams;
 // each chunk is H2D (bytes + offsets) -> kernel (offsets rebased by off0) ->

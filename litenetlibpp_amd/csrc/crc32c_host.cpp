@@ -23,6 +23,7 @@
 #endif
 
 #include "../../include/lnl_crc32c.h"
+#include "lnl_packet.h"
 
 namespace {
 
@@ -125,4 +126,15 @@ extern "C" int64_t lnl_crc32c_layer_inbound(const uint8_t* data, size_t length) 
     const uint32_t stored = (uint32_t)data[body] | ((uint32_t)data[body + 1] << 8) |
                             ((uint32_t)data[body + 2] << 16) | ((uint32_t)data[body + 3] << 24);
     return lnl_crc32c(data, body) == stored ? (int64_t)body : -1;
+}
+
+extern "C" int lnl_packet_verify(const uint8_t* data, size_t size) {
+    if (!data || size == 0) return 0;
+    return lnl_packet_verify_hdr(data[0], size) ? 1 : 0;
+}
+
+extern "C" int lnl_inbound_status(const uint8_t* data, size_t length) {
+    const int64_t body = lnl_crc32c_layer_inbound(data, length);
+    if (body < 0) return LNL_INBOUND_DROP_CRC;
+    return lnl_packet_verify(data, (size_t)body) ? LNL_INBOUND_ACCEPT : LNL_INBOUND_MALFORMED;
 }

@@ -20,6 +20,7 @@ struct BatchArgs {
     uint32_t n;            // datagrams
     uint32_t* out;         // CRC per datagram (may be null in Verify mode)
     uint8_t* ok;           // Verify mode: 1 = trailing CRC matches
+    uint32_t filter;       // Verify mode: ok = 2 when the CRC matches but net_packet::verify fails (lnl_packet.h)
     const uint8_t* dummy;  // 16 readable bytes (library scratch) for idle glds lanes
     const uint32_t* fold;  // LNL_TABLE_WORDS words from lnl_build_tables (device)
     const uint32_t* perm;  // optional: lane datagrams perm[64 b + lane] (pair / segment leftovers)
@@ -180,6 +181,7 @@ struct VerifyArgs {
     uint32_t n;
     const uint32_t* wire;  // CRC-32C of each whole datagram
     uint8_t* ok;
+    uint32_t filter;       // as BatchArgs::filter
     uint32_t* crc;         // optional
 };
 

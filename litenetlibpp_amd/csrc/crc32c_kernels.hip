@@ -47,6 +47,7 @@
 
 #include "crc32c_device.h"
 #include "crc32c_kernels.h"
+#include "lnl_packet.h"
 
 // Build knobs (defaults are the shipped configuration):
 //   LNL_GLDS_AUX   cache-policy bits of the LDS-DMA loads (0 = default, 2 = nt)
@@ -239,6 +240,9 @@ __device__ LNL_INLINE void store_result(const BatchArgs& a, const Batch& B, uint
             const uint32_t stored = (uint32_t)tail[0] | ((uint32_t)tail[1] << 8) |
                                     ((uint32_t)tail[2] << 16) | ((uint32_t)tail[3] << 24);
             ok = stored == crc;
+            // inbound filter: the CRC layer passed it, now net_packet::verify()
+            // on the stripped packet (net_manager.cpp:343)
+            if (ok && a.filter) ok = lnl_packet_verify_hdr(a.base[a.off[B.p] - a.off0], total - 4u) ? 1u : 2u;
         }
         a.ok[B.p] = (uint8_t)ok;
         if (a.out) a.out[B.p] = crc;

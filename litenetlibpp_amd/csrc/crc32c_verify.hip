@@ -11,12 +11,14 @@
 //   crc = CRC(body) = step^-32(CRC(wire) ^ ~0) ^ X ^ ~0, X = the stored LE32
 //         (register model: reg(M || X) = step^32(reg(M) ^ X) for 4 bytes X)
 //
-// matching the batch kernel's verify mode (crc 0 and ok 0 for len < 5).
+// matching the batch kernel's verify mode (crc 0 and ok 0 for len < 5; with
+// `filter`, ok 2 for a matching CRC whose packet fails net_packet::verify).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "crc32c_bitslice.h"
 #include "crc32c_kernels.h"
+#include "lnl_packet.h"
 
 namespace lnl {
 
@@ -31,7 +33,9 @@ __global__ __launch_bounds__(256) void verify_from_wire_kernel(VerifyArgs a) {
     const uint64_t total = e - s;
     const uint32_t wire = a.wire[i];
     const bool big = total >= 5u;
-    a.ok[i] = (uint8_t)(big && wire == kResidue ? 1u : 0u);
+    uint32_t ok = big && wire == kResidue ? 1u : 0u;
+    if (ok && a.filter) ok = lnl_packet_verify_hdr(a.base[s - a.off0], total - 4u) ? 1u : 2u;
+    a.ok[i] = (uint8_t)ok;
     if (a.crc) {
         uint32_t c = 0;
         if (big) {

@@ -83,3 +83,53 @@ def batch_csr(data: np.ndarray, offsets: np.ndarray, threads: int = 0, bitwise: 
     else:
         load().oracle_batch_csr(data.ctypes.data, off.ctypes.data, n, out.ctypes.data, threads)
     return out
+
+
+# ---- packet acceptance after the CRC layer ----------------------------------
+# net_packet::verify() (/root/reference/include/lnl/net_packet.h:120-131) over
+# HEADER_SIZES (:20-38: 17 initialisers for 18 properties, so index 17 is 0)
+# with net_constants.h:16-20 (HEADER_SIZE 1, CHANNELED 4, CONNECT_REQUEST 18,
+# CONNECT_ACCEPT 15, FRAGMENT_HEADER_SIZE 6).  Pinned to the reference's own
+# compiled header by tests/golden/packet_verify.bin.
+HEADER_SIZES = [1, 4, 4, 3, 11, 18, 15, 9, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0]
+FRAGMENT_HEADER_SIZE = 6
+INBOUND_DROP_CRC, INBOUND_ACCEPT, INBOUND_MALFORMED = 0, 1, 2
+
+
+def packet_verify(b0: int, size: int) -> bool:
+    """verify() of a packet whose byte 0 is b0 and whose size is `size` (size 0:
+    the reference reads byte 0 of its zeroed pool buffer, property 0 -> False)."""
+    if size == 0:
+        b0 = 0
+    prop = b0 & 0x1F
+    if prop >= len(HEADER_SIZES):
+        return False
+    hs = HEADER_SIZES[prop]
+    return size >= hs and (not (b0 & 0x80) or size >= hs + FRAGMENT_HEADER_SIZE)
+
+
+def inbound_status(wire: np.ndarray) -> int:
+    """Layer check (length >= 5, trailing LE32 == CRC-32C of the rest), then
+    verify() of the stripped packet (net_manager.cpp:218-222, :343)."""
+    w = np.ascontiguousarray(wire, dtype=np.uint8)
+    if w.size < 5:
+        return INBOUND_DROP_CRC
+    if crc(w[:-4]) != int(w[-4:].view("<u4")[0]):
+        return INBOUND_DROP_CRC
+    return INBOUND_ACCEPT if packet_verify(int(w[0]), w.size - 4) else INBOUND_MALFORMED
+
+
+REF_PACKET_SO = os.path.join(ORACLE_DIR, "_ref", "libref_packet.so")
+
+
+def load_ref_packet():
+    """The reference's own net_packet compiled by `make -C oracle ref`
+    (oracle/_ref/libref_packet.so), or None where it was not built."""
+    if not os.path.exists(REF_PACKET_SO):
+        return None
+    L = ctypes.CDLL(REF_PACKET_SO)
+    L.ref_packet_verify.restype = ctypes.c_int
+    L.ref_packet_verify.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    L.ref_packet_header_size.restype = ctypes.c_int
+    L.ref_packet_header_size.argtypes = [ctypes.c_uint8]
+    return L

@@ -304,6 +304,42 @@ def test_verify_mode_bucketed(P, csr_path):
     assert np.array_equal(u32(crc)[big], want_crc[big])
 
 
+def _wire_batch(rng, n, corrupt_frac=0.2):
+    """n wire datagrams (body || LE32 CRC) with random header bytes and short
+    bodies around every verify() threshold (empty bodies give 4-byte runts),
+    some corrupted."""
+    lens = np.where(rng.random(n) < 0.5, rng.integers(0, 30, n), rng.integers(0, 1429, n))
+    bodies = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    wire = np.empty(int(lens.sum()) + 4 * n, np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    pos = bpos = 0
+    for i, L in enumerate(lens):
+        body = bodies[bpos:bpos + L]
+        bpos += L
+        wire[pos:pos + L] = body
+        wire[pos + L:pos + L + 4] = np.frombuffer(np.uint32(oracle.crc(body)).tobytes(), np.uint8)
+        if rng.random() < corrupt_frac:
+            wire[pos + int(rng.integers(0, L + 4))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        pos += L + 4
+        off[i + 1] = pos
+    return wire, off
+
+
+@pytest.mark.parametrize("n", [1000, 40000])
+@all_paths
+def test_inbound_filter(P, csr_path, n):
+    """lnl_inbound_filter_csr_dev: CRC layer, then net_packet::verify() of the
+    stripped packet (reference-pinned restatement, tests/test_packet_verify.py),
+    per datagram, on every CSR path (n = 1000 takes the unbucketed kernel)."""
+    rng = np.random.default_rng(77 + n)
+    wire, off = _wire_batch(rng, n)
+    exp = np.array([oracle.inbound_status(wire[int(off[i]):int(off[i + 1])]) for i in range(n)], np.uint8)
+    got = P.inbound_filter(dev(wire), dev(off.view(np.int64), torch.int64)).cpu().numpy()
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}: got {got[bad[:5]]} exp {exp[bad[:5]]}"
+    assert set(np.unique(exp)) == {0, 1, 2}
+
+
 @all_paths
 def test_full_config3_bit_exact(P, csr_path):
     # BASELINE config 3 at full size: 2^20 datagrams of 64..1400 B, CSR
