@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 3
+#define LNL_CRC32C_ABI_VERSION 4
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -127,6 +127,26 @@ int lnl_inbound_filter_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uin
  * PCIe rate; pageable ones work but copy through a staging buffer. */
 int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                           uint32_t* h_out, int device);
+
+/* Host-resident inbound filter (lnl_inbound_filter_csr_dev over a pinned host
+ * burst, same chunked two-stream pipeline as lnl_crc32c_batch_host): writes
+ * h_status[i] (LNL_INBOUND_*), blocks until done. */
+int lnl_inbound_filter_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
+                            uint8_t* h_status, int device);
+
+/* Batched socket ingress (CPU): one recvmmsg call pulls up to max_n datagrams
+ * from the UDP socket fd into LNL_INGRESS_SLOT-byte slots of buf (cap bytes;
+ * pinned memory for the GPU batch that follows), then compacts them in place
+ * to a CSR burst: datagram i = buf[off[i] .. off[i+1]), off[0] = 0 (off has
+ * max_n + 1 entries).  addrs (optional) receives max_n struct sockaddr_in
+ * senders.  wait_ms != 0 polls first (-1: forever), like the reference's
+ * receive loop (/root/reference/src/lnl/net_manager.cpp:202-223); 0 never
+ * blocks.  Returns the number of datagrams (0: none ready), or a negative
+ * errno.  Longer datagrams are truncated to the slot, as recvfrom into the
+ * reference's MAX_PACKET_SIZE packet truncates them. */
+#define LNL_INGRESS_SLOT 1432
+int lnl_ingress_recv_batch(int fd, uint8_t* buf, size_t cap, uint64_t* off, uint32_t max_n, void* addrs,
+                           int wait_ms);
 
 /* Multi-device form of lnl_crc32c_batch_host: the batch
  * is split into ndev contiguous datagram ranges of ceil(n / ndev) (the last

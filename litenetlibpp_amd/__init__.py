@@ -13,6 +13,9 @@ from .crc32c import (  # noqa: F401
     batch_host,
     batch_host_multi,
     inbound_filter,
+    inbound_filter_host,
+    ingress_recv_batch,
+    INGRESS_SLOT,
     inbound_status,
     packet_verify,
     INBOUND_ACCEPT,

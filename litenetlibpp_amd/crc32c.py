@@ -21,6 +21,7 @@ uint32 bit patterns (use ``.cpu().numpy().view(np.uint32)``).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import numpy as np
@@ -33,7 +34,8 @@ HEADER_SIZE = 1        # net_constants::HEADER_SIZE (/root/reference/include/lnl
 __all__ = [
     "Crc32cError", "EXTRA_PACKET_SIZE", "crc32c", "crc32c_extend", "Crc32cLayer",
     "batch_fixed", "batch_csr", "verify_csr", "batch_host", "batch_host_multi", "mtu_with_layer",
-    "packet_verify", "inbound_status", "inbound_filter",
+    "packet_verify", "inbound_status", "inbound_filter", "inbound_filter_host", "ingress_recv_batch",
+    "INGRESS_SLOT",
     "INBOUND_DROP_CRC", "INBOUND_ACCEPT", "INBOUND_MALFORMED",
 ]
 
@@ -211,6 +213,34 @@ def inbound_filter(data, offsets, stream=None):
         check(lib().lnl_inbound_filter_csr_dev(data.data_ptr(), offsets.data_ptr(), n, status.data_ptr(),
                                                _stream_handle(stream)), "lnl_inbound_filter_csr_dev")
     return status
+
+
+def inbound_filter_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
+    """Host-resident burst through the GPU inbound filter (H2D -> filter ->
+    D2H on 2 streams).  Blocking.  Returns uint8 status codes."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets).astype(np.uint64, copy=False)
+    n = offsets.size - 1
+    out = np.empty(max(n, 0), dtype=np.uint8)
+    if n > 0:
+        check(lib().lnl_inbound_filter_host(data.ctypes.data, offsets.ctypes.data, n, out.ctypes.data, device),
+              "lnl_inbound_filter_host")
+    return out
+
+
+INGRESS_SLOT = 1432  # LNL_INGRESS_SLOT: bytes per datagram slot (the reference's MAX_PACKET_SIZE)
+
+
+def ingress_recv_batch(fd: int, buf: np.ndarray, max_n: int, wait_ms: int = 0):
+    """One recvmmsg burst from UDP socket fd into buf (uint8, ideally pinned),
+    compacted to CSR.  Returns (n, offsets[n + 1]); n = 0 when nothing was ready."""
+    if buf.dtype != np.uint8 or not buf.flags["C_CONTIGUOUS"]:
+        raise ValueError("buf must be a contiguous uint8 array")
+    off = np.zeros(max_n + 1, dtype=np.uint64)
+    r = lib().lnl_ingress_recv_batch(fd, buf.ctypes.data, buf.nbytes, off.ctypes.data, max_n, None, wait_ms)
+    if r < 0:
+        raise Crc32cError(r, "lnl_ingress_recv_batch", os.strerror(-r))
+    return r, off[: r + 1]
 
 
 def batch_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:

@@ -498,8 +498,12 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
 // each chunk is H2D (bytes + offsets) -> kernel (offsets rebased by off0) ->
 // D2H (CRCs).  Stream order makes buffer reuse safe; the two streams overlap
 // one chunk's copies with the other's kernel.
-extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
-                                     uint32_t* h_out, int device) {
+namespace {
+// Host-resident CSR batch through `device` (lnl_crc32c_batch_host and
+// lnl_inbound_filter_host): chunks over two streams, H2D -> kernel -> D2H.
+// filter = 0: h_out is u32 CRCs; 1: h_out is u8 inbound status codes.
+int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h_out, int device,
+               uint32_t filter) {
     if (n == 0) return 0;
     if (!h_base || !h_off || !h_out) return fail(-EINVAL, "NULL argument");
     for (uint32_t i = 0; i < n; ++i)
@@ -576,10 +580,17 @@ extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_of
         a.off = S->d_off[k];
         a.off0 = h_off[i];
         a.n = cn;
-        a.out = S->d_out[k];
-        if (int rc = launch_csr(*S, a, lnl::kModeCsr, st)) return rc;
-        if ((e = hipMemcpyAsync(h_out + i, S->d_out[k], (size_t)cn * 4, hipMemcpyDeviceToHost, st)) !=
-            hipSuccess)
+        const size_t esz = filter ? 1 : 4;  // bytes of output per datagram
+        if (filter) {
+            a.ok = (uint8_t*)S->d_out[k];
+            a.filter = 1;
+            if (int rc = launch_csr(*S, a, lnl::kModeVerify, st)) return rc;
+        } else {
+            a.out = S->d_out[k];
+            if (int rc = launch_csr(*S, a, lnl::kModeCsr, st)) return rc;
+        }
+        if ((e = hipMemcpyAsync((uint8_t*)h_out + (size_t)i * esz, S->d_out[k], (size_t)cn * esz,
+                                hipMemcpyDeviceToHost, st)) != hipSuccess)
             return hip_fail(e, "D2H");
         i = j;
         k ^= 1;
@@ -587,6 +598,17 @@ extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_of
     for (int s = 0; s < 2; ++s)
         if ((e = hipStreamSynchronize(S->streams[s])) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     return 0;
+}
+}  // namespace
+
+extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
+                                     uint32_t* h_out, int device) {
+    return host_batch(h_base, h_off, n, h_out, device, 0u);
+}
+
+extern "C" int lnl_inbound_filter_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
+                                       uint8_t* h_status, int device) {
+    return host_batch(h_base, h_off, n, h_status, device, 1u);
 }
 
 extern "C" int lnl_crc32c_batch_host_multi(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,

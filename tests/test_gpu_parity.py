@@ -461,6 +461,44 @@ def test_host_multi_device_path(P, devices):
     assert np.array_equal(got, oracle.batch_csr(data, off))
 
 
+def test_socket_path_end_to_end(P):
+    """Config 5 over real sockets: wire datagrams sent over UDP loopback,
+    received in recvmmsg bursts into a pinned buffer (lnl_ingress_recv_batch),
+    filtered on the GPU (lnl_inbound_filter_host) -- statuses equal the
+    oracle's per datagram."""
+    import socket
+    rng = np.random.default_rng(55)
+    rx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 23)
+    rx.bind(("127.0.0.1", 0))
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    tx.connect(rx.getsockname())
+    layer = P.Crc32cLayer()
+    sent = []
+    for i in range(3000):
+        body = rng.integers(0, 256, int(rng.integers(0, 1428)), dtype=np.uint8)
+        if body.size:
+            body[0] = rng.choice([0x00, 0x01, 0x81, 0x05, 0x1F])
+        w = bytearray(layer.process_outbound(body.tobytes()))
+        if i % 17 == 0:
+            w[int(rng.integers(0, len(w)))] ^= 0x10
+        sent.append(bytes(w))
+        tx.send(bytes(w))
+    burst = 256
+    buf = torch.empty(burst * P.INGRESS_SLOT, dtype=torch.uint8).pin_memory().numpy()
+    got_status, got_wire = [], []
+    while len(got_wire) < len(sent):
+        n, off = P.ingress_recv_batch(rx.fileno(), buf, burst, wait_ms=2000)
+        assert n > 0, f"timed out after {len(got_wire)}"
+        got_status += list(P.inbound_filter_host(buf, off, 0))
+        got_wire += [bytes(buf[int(off[i]):int(off[i + 1])]) for i in range(n)]
+    rx.close()
+    tx.close()
+    assert got_wire == sent
+    exp = [oracle.inbound_status(np.frombuffer(w, np.uint8)) for w in sent]
+    assert got_status == exp and set(exp) == {0, 1, 2}
+
+
 def test_full_config2_bit_exact(P):
     # BASELINE config 2 at full size: 2^20 x 1400 B, every CRC compared
     n, L = 1 << 20, 1400
