@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 4
+#define LNL_CRC32C_ABI_VERSION 5
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -127,6 +127,19 @@ int lnl_inbound_filter_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uin
  * PCIe rate; pageable ones work but copy through a staging buffer. */
 int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                           uint32_t* h_out, int device);
+
+/* The packets a filtered burst delivers: for every
+ * datagram with d_status[i] == LNL_INBOUND_ACCEPT, either the datagram itself
+ * without its CRC, or -- for a MERGED container (property 12) -- the packets
+ * it carries, cut as net_peer::process_packet does
+ * (/root/reference/src/lnl/net_peer.cpp:164-187: [u16 LE size][packet]...,
+ * stopping at the first packet net_packet::verify rejects or that runs past
+ * the datagram).  Packet k: base[d_pkt_start[k] .. + d_pkt_len[k]) from
+ * datagram d_pkt_parent[k], in datagram order.  *d_total (device) receives
+ * the number of packets; only the first `cap` are written.  Stream-ordered. */
+int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, const uint8_t* d_status,
+                         uint64_t* d_pkt_start, uint32_t* d_pkt_len, uint32_t* d_pkt_parent, uint32_t cap,
+                         uint32_t* d_total, void* hip_stream);
 
 /* Host-resident inbound filter (lnl_inbound_filter_csr_dev over a pinned host
  * burst, same chunked two-stream pipeline as lnl_crc32c_batch_host): writes

@@ -12,6 +12,7 @@ from .crc32c import (  # noqa: F401
     batch_fixed,
     batch_host,
     batch_host_multi,
+    dispatch,
     inbound_filter,
     inbound_filter_host,
     ingress_recv_batch,

@@ -35,6 +35,7 @@ __all__ = [
     "Crc32cError", "EXTRA_PACKET_SIZE", "crc32c", "crc32c_extend", "Crc32cLayer",
     "batch_fixed", "batch_csr", "verify_csr", "batch_host", "batch_host_multi", "mtu_with_layer",
     "packet_verify", "inbound_status", "inbound_filter", "inbound_filter_host", "ingress_recv_batch",
+    "dispatch",
     "INGRESS_SLOT",
     "INBOUND_DROP_CRC", "INBOUND_ACCEPT", "INBOUND_MALFORMED",
 ]
@@ -213,6 +214,36 @@ def inbound_filter(data, offsets, stream=None):
         check(lib().lnl_inbound_filter_csr_dev(data.data_ptr(), offsets.data_ptr(), n, status.data_ptr(),
                                                _stream_handle(stream)), "lnl_inbound_filter_csr_dev")
     return status
+
+
+def dispatch(data, offsets, status, cap: Optional[int] = None, stream=None):
+    """Packets a filtered burst delivers, on the GPU: accepted datagrams (CRC
+    stripped) and the packets of MERGED containers.  Returns (start int64,
+    length int32, parent int32) tensors of the delivered packets (all of them
+    when cap is None: a first call counts, a second fills)."""
+    torch = _torch()
+    _check_dev_u8(data, "data")
+    _check_off(offsets, data)
+    n = offsets.numel() - 1
+    dev = data.device
+    total = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def run(c):
+        start = torch.empty(max(c, 1), dtype=torch.int64, device=dev)
+        length = torch.empty(max(c, 1), dtype=torch.int32, device=dev)
+        parent = torch.empty(max(c, 1), dtype=torch.int32, device=dev)
+        check(lib().lnl_dispatch_csr_dev(data.data_ptr(), offsets.data_ptr(), max(n, 0), status.data_ptr(),
+                                         start.data_ptr(), length.data_ptr(), parent.data_ptr(), c,
+                                         total.data_ptr(), _stream_handle(stream)), "lnl_dispatch_csr_dev")
+        return start, length, parent
+
+    start, length, parent = run(cap if cap is not None else 0)
+    t = int(total.item())
+    if cap is None:
+        start, length, parent = run(t)
+        cap = t
+    k = min(t, cap)
+    return start[:k], length[:k], parent[:k]
 
 
 def inbound_filter_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:

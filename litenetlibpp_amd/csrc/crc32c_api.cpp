@@ -611,6 +611,45 @@ extern "C" int lnl_inbound_filter_host(const uint8_t* h_base, const uint64_t* h_
     return host_batch(h_base, h_off, n, h_status, device, 1u);
 }
 
+extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                    const uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
+                                    uint32_t* d_pkt_parent, uint32_t cap, uint32_t* d_total, void* hip_stream) {
+    if (!d_total) return fail(-EINVAL, "d_total is NULL");
+    hipStream_t st = (hipStream_t)hip_stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_total, 0, 4, st);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
+    if (!d_base || !d_off || !d_status) return fail(-EINVAL, "NULL argument");
+    if (cap && (!d_pkt_start || !d_pkt_len || !d_pkt_parent)) return fail(-EINVAL, "NULL output");
+    DeviceState* S;
+    if (int rc = current_device(&S)) return rc;
+    const size_t scan_bytes = lnl::dispatch_scan_bytes(n);
+    void* scratch = nullptr;
+    const size_t bytes = 2 * (size_t)n * 4 + scan_bytes + 256;
+    hipError_t e = hipMallocAsync(&scratch, bytes, st);
+    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
+    lnl::DispatchArgs a{};
+    a.base = d_base;
+    a.off = d_off;
+    a.n = n;
+    a.status = d_status;
+    a.counts = (uint32_t*)scratch;
+    a.first = a.counts + n;
+    a.pkt_start = d_pkt_start;
+    a.pkt_len = d_pkt_len;
+    a.pkt_parent = d_pkt_parent;
+    a.cap = cap;
+    a.total = d_total;
+    void* tmp = (void*)(((uintptr_t)(a.first + n) + 255) & ~(uintptr_t)255);
+    int rc = 0;
+    e = lnl::launch_dispatch(a, tmp, scan_bytes, st);
+    if (e != hipSuccess) rc = hip_fail(e, "dispatch launch");
+    e = hipFreeAsync(scratch, st);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
+}
+
 extern "C" int lnl_crc32c_batch_host_multi(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                                            uint32_t* h_out, const int* devices, int ndev) {
     if (n == 0) return 0;

@@ -173,6 +173,25 @@ void csr_plan_layout(CsrPlanArgs& a, uint32_t* scratch);
 // zeroes the counters, then plan count / plan scatter / uniform kernel
 hipError_t launch_csr_uniform(const CsrPlanArgs& p, const CsrArgs& c, int grid, hipStream_t stream);
 
+// Delivered packets of a filtered burst (lnl_dispatch.hip): accepted
+// datagrams, MERGED containers cut into their packets.
+struct DispatchArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    uint64_t off0;
+    uint32_t n;
+    const uint8_t* status;  // lnl_inbound_filter output
+    uint32_t* counts;       // n (scratch)
+    uint32_t* first;        // n (scratch): exclusive scan of counts
+    uint64_t* pkt_start;    // cap: packet start relative to base
+    uint32_t* pkt_len;      // cap
+    uint32_t* pkt_parent;   // cap: datagram index
+    uint32_t cap;
+    uint32_t* total;        // device: packets delivered (may exceed cap)
+};
+size_t dispatch_scan_bytes(uint32_t n);
+hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
+
 // Verify epilogue (crc32c_verify.hip): ok / body CRC from wire-datagram CRCs.
 struct VerifyArgs {
     const uint8_t* base;

@@ -133,3 +133,33 @@ def load_ref_packet():
     L.ref_packet_header_size.restype = ctypes.c_int
     L.ref_packet_header_size.argtypes = [ctypes.c_uint8]
     return L
+
+
+MERGED_PROPERTY = 12  # PACKET_PROPERTY::MERGED (net_enums.h:60)
+
+
+def dispatch(wire_list, status):
+    """Packets a filtered burst delivers: (datagram index, offset within the
+    datagram, length) per packet.  Accepted datagrams are one packet (CRC
+    stripped); a MERGED container is cut as net_peer::process_packet does
+    (/root/reference/src/lnl/net_peer.cpp:164-187), bounded by the datagram
+    (the reference bounds by its pool buffer and reads stale bytes past it)."""
+    out = []
+    for i, (w, st) in enumerate(zip(wire_list, status)):
+        if st != INBOUND_ACCEPT:
+            continue
+        size = len(w) - 4
+        if w[0] & 0x1F != MERGED_PROPERTY:
+            out.append((i, 0, size))
+            continue
+        pos = 1
+        while pos < size:
+            if pos + 2 > size:
+                break
+            L = int(w[pos]) | (int(w[pos + 1]) << 8)
+            pos += 2
+            if L > size - pos or L == 0 or not packet_verify(int(w[pos]), L):
+                break
+            out.append((i, pos, L))
+            pos += L
+    return out

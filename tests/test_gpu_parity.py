@@ -499,6 +499,65 @@ def test_socket_path_end_to_end(P):
     assert got_status == exp and set(exp) == {0, 1, 2}
 
 
+def _merged(rng, parts, mode):
+    """A MERGED container (header 0x0C) of sub-packets as net_peer::send_merged
+    lays them out ([u16 LE size][packet]...), optionally damaged."""
+    out = bytearray([0x0C])
+    for body in parts:
+        out += len(body).to_bytes(2, "little") + body
+    if mode == "truncated" and len(out) > 4:
+        out = out[: int(rng.integers(2, len(out)))]
+    elif mode == "bad_sub" and parts:
+        k = 1 + 2                                      # first sub-packet's header byte
+        out[k] = 0x1F                                  # unknown property: verify() fails
+    elif mode == "zero_len":
+        out += (0).to_bytes(2, "little") + bytes([0x00, 0x01])
+    return bytes(out)
+
+
+@pytest.mark.parametrize("n", [500, 30000])
+def test_dispatch_merged_containers(P, n):
+    """lnl_dispatch_csr_dev after lnl_inbound_filter_csr_dev: accepted
+    datagrams and the packets of MERGED containers (well-formed, truncated,
+    with a rejected sub-packet, a zero-length entry, nested), in datagram
+    order, against oracle.dispatch (net_peer.cpp:164-187 restated)."""
+    rng = np.random.default_rng(900 + n)
+    layer = P.Crc32cLayer()
+    wires = []
+    for i in range(n):
+        r = rng.random()
+        if r < 0.5:
+            parts = [bytes([int(rng.choice([0x00, 0x01, 0x03]))]) +
+                     rng.integers(0, 256, int(rng.integers(3, 60)), dtype=np.uint8).tobytes()
+                     for _ in range(int(rng.integers(0, 12)))]
+            mode = rng.choice(["ok", "ok", "ok", "truncated", "bad_sub", "zero_len"])
+            body = _merged(rng, parts, mode)
+            if rng.random() < 0.05:                        # nested container: delivered whole
+                body = _merged(rng, [body], "ok")
+        else:
+            body = bytes([int(rng.choice([0x00, 0x01, 0x1F]))]) + \
+                rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes()
+        w = bytearray(layer.process_outbound(body))
+        if rng.random() < 0.03:
+            w[int(rng.integers(0, len(w)))] ^= 0x04
+        wires.append(bytes(w))
+    off = np.concatenate([[0], np.cumsum([len(w) for w in wires])]).astype(np.uint64)
+    blob = np.frombuffer(b"".join(wires), np.uint8)
+    d, o = dev(blob), dev(off.view(np.int64), torch.int64)
+    status = P.inbound_filter(d, o)
+    start, length, parent = P.dispatch(d, o, status)
+    st = status.cpu().numpy()
+    exp = oracle.dispatch([np.frombuffer(w, np.uint8) for w in wires], st)
+    got = list(zip(parent.cpu().numpy().tolist(),
+                   (start.cpu().numpy() - off[parent.cpu().numpy()].astype(np.int64)).tolist(),
+                   length.cpu().numpy().tolist()))
+    assert got == exp
+    assert any(L for (_, pos, L) in exp if pos > 0)        # some container packets delivered
+    # a capped call writes the first `cap` packets and still reports the total
+    s2, l2, p2 = P.dispatch(d, o, status, cap=7)
+    assert p2.cpu().numpy().tolist() == [e[0] for e in exp[:7]]
+
+
 def test_full_config2_bit_exact(P):
     # BASELINE config 2 at full size: 2^20 x 1400 B, every CRC compared
     n, L = 1 << 20, 1400
