@@ -13,7 +13,8 @@ a MAX over per-rank times).  Inputs are generated on the device before the
 timed region.  Rank 0 prints ONE JSON line.
 
 roofline: algorithmic bytes per launch = sum(L) + 4 N (datagram bytes read +
-CRC words written; CSR adds 8 N offset bytes) over the average launch duration
+CRC words written; CSR adds 8 N offset bytes; the xor workload reads and writes
+2 sum(L)) over the average launch duration
 measured with one HIP event pair around the K launches on the launch stream;
 peak 8.0 TB/s (MI355X HBM3E nameplate).  traffic: HBM bytes per launch from the rocprofv3 PMC pass
 (profiles/traffic_<workload>.json, FETCH_SIZE x2 gfx950 correction +
@@ -48,7 +49,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["fixed", "csr"], default="fixed")
+    ap.add_argument("--workload", choices=["fixed", "csr", "xor"], default="fixed",
+                    help="fixed: config 2 (the headline); csr: config 3; xor: the XOR-encryption "
+                         "layer in place over the config-2 batch (SURVEY 8(f) item 4)")
     ap.add_argument("--packets", type=int, default=1 << 20, help="per GPU")
     ap.add_argument("--length", type=int, default=1400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -63,6 +66,10 @@ def make_workload(args, rank, world, device):
     g = torch.Generator(device=device)
     g.manual_seed(42 + rank)
     _, n = shard_range(args.packets * world, rank, world)
+    if args.workload == "xor":  # read + write every byte in place
+        L = args.length
+        data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
+        return dict(data=data, n=n, L=L, off=None, payload=n * L, algo=2 * n * L, xor=True)
     if args.workload == "fixed":
         L = args.length
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
@@ -76,8 +83,13 @@ def make_workload(args, rank, world, device):
     return dict(data=data, n=n, L=None, off=off, payload=total, algo=total + 4 * n + 8 * (n + 1))
 
 
+XOR_KEY = b"LiteNetLibPP-bench-key"
+
+
 def launch(P, w, out, stream):
-    if w["off"] is None:
+    if w.get("xor"):
+        P.xor_layer_fixed(w["data"], w["L"], w["L"], w["n"], XOR_KEY, stream=stream)
+    elif w["off"] is None:
         P.batch_fixed(w["data"], w["L"], w["L"], w["n"], out=out, stream=stream)
     else:
         P.batch_csr(w["data"], w["off"], out=out, stream=stream)
@@ -203,7 +215,9 @@ def main():
             with open(tf) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         line = {
-            "metric": METRIC if args.workload == "fixed" else "CRC32C GB/s (device-resident) over 1M mixed-length (64-1400B) packets; bit-exact",
+            "metric": {"fixed": METRIC,
+                       "csr": "CRC32C GB/s (device-resident) over 1M mixed-length (64-1400B) packets; bit-exact",
+                       "xor": "XOR-layer GB/s (device-resident, in place) over 1M x 1400B packets"}[args.workload],
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -216,9 +230,9 @@ def main():
             "dtype": "u8",
             "data": "synthetic (torch.randint on device, seed 42+rank), resident in HBM before timing",
             "config": {
-                "workload": ("config2: 2^20 x 1400 B datagrams per GPU, fixed stride 1400, device-resident"
-                             if args.workload == "fixed" else
-                             "config3: 2^20 mixed-length datagrams (64..1400 B uniform) per GPU, CSR int64 offsets"),
+                "workload": {"fixed": "config2: 2^20 x 1400 B datagrams per GPU, fixed stride 1400, device-resident",
+                             "csr": "config3: 2^20 mixed-length datagrams (64..1400 B uniform) per GPU, CSR int64 offsets",
+                             "xor": "XOR layer over the config-2 batch, in place (22-byte key)"}[args.workload],
                 "packets_per_gpu": w["n"],
                 "payload_bytes_per_gpu": w["payload"],
                 "parallelism": f"shard{world} (contiguous packet ranges, no data-path collectives)",
@@ -237,7 +251,7 @@ def main():
         probe = hbm_probe_peak(w["data"], device)
         if probe:
             line["roofline"]["measured_stream_read_peak_gbs"] = round(probe, 1)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not w.get("xor"):
             gpu_out = out.cpu().numpy().view(np.uint32)
             res, threads, desc, exact = cpu_baseline(w, gpu_out)
             line["cpu_baseline"] = {

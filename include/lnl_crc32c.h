@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 5
+#define LNL_CRC32C_ABI_VERSION 6
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -140,6 +140,18 @@ int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t
 int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, const uint8_t* d_status,
                          uint64_t* d_pkt_start, uint32_t* d_pkt_len, uint32_t* d_pkt_parent, uint32_t cap,
                          uint32_t* d_total, void* hip_stream);
+
+/* Upstream LiteNetLib's XOR-encryption layer (XorEncryptLayer; SURVEY.md 8(f)
+ * item 4), in place: data[i] ^= key[i % key_len] for i < length, the key phase
+ * restarting at every datagram.  Both directions are the same map; the layer
+ * adds no bytes.  key_len 1 .. LNL_XOR_MAX_KEY. */
+#define LNL_XOR_MAX_KEY 256
+int lnl_xor_layer(uint8_t* data, size_t length, const uint8_t* key, size_t key_len);
+/* The same over every datagram of a device batch (stream-ordered). */
+int lnl_xor_layer_csr_dev(uint8_t* d_base, const uint64_t* d_off, uint32_t n, const uint8_t* key,
+                          size_t key_len, void* hip_stream);
+int lnl_xor_layer_fixed_dev(uint8_t* d_base, size_t stride, uint32_t len, uint32_t n, const uint8_t* key,
+                            size_t key_len, void* hip_stream);
 
 /* Host-resident inbound filter (lnl_inbound_filter_csr_dev over a pinned host
  * burst, same chunked two-stream pipeline as lnl_crc32c_batch_host): writes

@@ -13,6 +13,9 @@ from .crc32c import (  # noqa: F401
     batch_host,
     batch_host_multi,
     dispatch,
+    xor_layer,
+    xor_layer_csr,
+    xor_layer_fixed,
     inbound_filter,
     inbound_filter_host,
     ingress_recv_batch,

@@ -35,7 +35,7 @@ __all__ = [
     "Crc32cError", "EXTRA_PACKET_SIZE", "crc32c", "crc32c_extend", "Crc32cLayer",
     "batch_fixed", "batch_csr", "verify_csr", "batch_host", "batch_host_multi", "mtu_with_layer",
     "packet_verify", "inbound_status", "inbound_filter", "inbound_filter_host", "ingress_recv_batch",
-    "dispatch",
+    "dispatch", "xor_layer", "xor_layer_csr", "xor_layer_fixed",
     "INGRESS_SLOT",
     "INBOUND_DROP_CRC", "INBOUND_ACCEPT", "INBOUND_MALFORMED",
 ]
@@ -244,6 +244,43 @@ def dispatch(data, offsets, status, cap: Optional[int] = None, stream=None):
         cap = t
     k = min(t, cap)
     return start[:k], length[:k], parent[:k]
+
+
+def _key(key) -> bytes:
+    k = key.encode("utf-8") if isinstance(key, str) else bytes(key)   # upstream SetKey(string): UTF-8
+    if not 1 <= len(k) <= 256:
+        raise ValueError("key must be 1..256 bytes")
+    return k
+
+
+def xor_layer(data: np.ndarray, key) -> None:
+    """Upstream XorEncryptLayer on one datagram, in place, on the CPU."""
+    k = _key(key)
+    if data.dtype != np.uint8 or not data.flags["C_CONTIGUOUS"]:
+        raise ValueError("data must be a contiguous uint8 array")
+    check(lib().lnl_xor_layer(data.ctypes.data, data.nbytes, k, len(k)), "lnl_xor_layer")
+
+
+def xor_layer_csr(data, offsets, key, stream=None) -> None:
+    """XorEncryptLayer over every datagram of a device CSR batch, in place."""
+    _check_dev_u8(data, "data")
+    _check_off(offsets, data)
+    k = _key(key)
+    n = offsets.numel() - 1
+    if n > 0:
+        check(lib().lnl_xor_layer_csr_dev(data.data_ptr(), offsets.data_ptr(), n, k, len(k),
+                                          _stream_handle(stream)), "lnl_xor_layer_csr_dev")
+
+
+def xor_layer_fixed(data, stride: int, length: int, n: int, key, stream=None) -> None:
+    """XorEncryptLayer over n datagrams at a fixed stride on the device, in place."""
+    _check_dev_u8(data, "data")
+    k = _key(key)
+    if n and (n - 1) * stride + length > data.numel():
+        raise ValueError("batch exceeds data")
+    if n > 0:
+        check(lib().lnl_xor_layer_fixed_dev(data.data_ptr(), stride, length, n, k, len(k),
+                                            _stream_handle(stream)), "lnl_xor_layer_fixed_dev")
 
 
 def inbound_filter_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:

@@ -650,6 +650,47 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     return rc;
 }
 
+namespace {
+int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t len, uint32_t n,
+              const uint8_t* key, size_t key_len, void* hip_stream) {
+    if (!key || key_len == 0 || key_len > lnl::kXorMaxKey)
+        return fail(-EINVAL, "key_len %zu outside 1..%u", key_len, lnl::kXorMaxKey);
+    if (n == 0) return 0;
+    if (!d_base) return fail(-EINVAL, "d_base is NULL");
+    DeviceState* S;
+    if (int rc = current_device(&S)) return rc;
+    lnl::XorArgs a{};
+    a.base = d_base;
+    a.off = d_off;
+    a.stride = stride;
+    a.len = len;
+    a.n = n;
+    a.key_len = (uint32_t)key_len;
+    memcpy(a.key, key, key_len);
+    // lnl::kXorPerWg datagrams per workgroup (uncapped grid: measured faster than persistent)
+    const uint32_t wgs = (n + lnl::kXorPerWg - 1u) / lnl::kXorPerWg;
+#ifndef LNL_XOR_WG_PER_CU
+#define LNL_XOR_WG_PER_CU 0  // 0: one workgroup per kXorPerWg datagrams, no cap
+#endif
+    const uint32_t cap = LNL_XOR_WG_PER_CU ? (uint32_t)S->cus * LNL_XOR_WG_PER_CU : 0xFFFFFFFFu;
+    const int grid = (int)std::max(1u, std::min(wgs, cap));
+    hipError_t e = lnl::launch_xor_layer(a, grid, (hipStream_t)hip_stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "xor layer launch");
+}
+}  // namespace
+
+extern "C" int lnl_xor_layer_csr_dev(uint8_t* d_base, const uint64_t* d_off, uint32_t n, const uint8_t* key,
+                                     size_t key_len, void* hip_stream) {
+    if (n && !d_off) return fail(-EINVAL, "d_off is NULL");
+    return xor_layer(d_base, d_off, 0, 0, n, key, key_len, hip_stream);
+}
+
+extern "C" int lnl_xor_layer_fixed_dev(uint8_t* d_base, size_t stride, uint32_t len, uint32_t n,
+                                       const uint8_t* key, size_t key_len, void* hip_stream) {
+    if (n && stride < len) return fail(-EINVAL, "stride %zu < len %u", stride, len);
+    return xor_layer(d_base, nullptr, stride, len, n, key, key_len, hip_stream);
+}
+
 extern "C" int lnl_crc32c_batch_host_multi(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                                            uint32_t* h_out, const int* devices, int ndev) {
     if (n == 0) return 0;

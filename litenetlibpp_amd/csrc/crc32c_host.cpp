@@ -11,6 +11,7 @@
 // threads (/root/reference/src/lnl/net_manager.cpp:106-107).  Uses the SSE4.2
 // crc32 instruction (which computes exactly CRC-32C) when the CPU has it, else
 // slicing-by-8 tables built at compile time.
+#include <errno.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
@@ -137,4 +138,14 @@ extern "C" int lnl_inbound_status(const uint8_t* data, size_t length) {
     const int64_t body = lnl_crc32c_layer_inbound(data, length);
     if (body < 0) return LNL_INBOUND_DROP_CRC;
     return lnl_packet_verify(data, (size_t)body) ? LNL_INBOUND_ACCEPT : LNL_INBOUND_MALFORMED;
+}
+
+extern "C" int lnl_xor_layer(uint8_t* data, size_t length, const uint8_t* key, size_t key_len) {
+    if (!key || key_len == 0 || key_len > LNL_XOR_MAX_KEY) return -EINVAL;
+    if (length && !data) return -EINVAL;
+    for (size_t i = 0, k = 0; i < length; ++i) {
+        data[i] ^= key[k];
+        if (++k == key_len) k = 0;
+    }
+    return 0;
 }

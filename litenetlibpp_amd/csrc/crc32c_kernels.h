@@ -173,6 +173,24 @@ void csr_plan_layout(CsrPlanArgs& a, uint32_t* scratch);
 // zeroes the counters, then plan count / plan scatter / uniform kernel
 hipError_t launch_csr_uniform(const CsrPlanArgs& p, const CsrArgs& c, int grid, hipStream_t stream);
 
+// XOR-encryption layer over a batch (lnl_xor.hip), in place.
+constexpr uint32_t kXorMaxKey = 256;
+#ifndef LNL_XOR_GROUP
+#define LNL_XOR_GROUP 32  // lanes per datagram (lnl_xor.hip)
+#endif
+constexpr uint32_t kXorPerWg = 256u / LNL_XOR_GROUP;  // datagrams a 256-thread workgroup works on at once
+struct XorArgs {
+    uint8_t* base;
+    const uint64_t* off;  // CSR offsets, or null: fixed stride
+    uint64_t off0;
+    uint64_t stride;
+    uint32_t len;
+    uint32_t n;
+    uint32_t key_len;     // 1 .. kXorMaxKey
+    uint8_t key[kXorMaxKey];
+};
+hipError_t launch_xor_layer(const XorArgs& a, int grid, hipStream_t stream);
+
 // Delivered packets of a filtered burst (lnl_dispatch.hip): accepted
 // datagrams, MERGED containers cut into their packets.
 struct DispatchArgs {

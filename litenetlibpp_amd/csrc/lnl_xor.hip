@@ -1,0 +1,140 @@
+// lnl_xor.hip -- upstream LiteNetLib's XOR-encryption packet layer over a
+// batch (unported by the reference, README.MD:35).
+//
+// Upstream XorEncryptLayer (C#, not available offline; restated):
+// ExtraPacketSizeForLayer = 0, and both directions do, per datagram,
+//
+//   for i in 0 .. length-1:  data[offset + i] ^= key[i % key.Length]
+//
+// i.e. the key phase restarts at every datagram's first byte.  The batch form
+// applies it in place to every datagram of a CSR or fixed-stride batch.
+//
+// HBM-bound byte map (reads and writes every datagram byte once): a group of
+// 32 lanes owns a datagram and walks its 16-byte pieces (aligned to the
+// buffer, so loads and stores are whole dwordx4, four per lane in flight,
+// except the partial first and last piece of each datagram: their other bytes
+// belong to the neighbouring datagrams, updated concurrently by other lanes,
+// so those pieces are read whole and written back byte by byte, own bytes
+// only.  One workgroup per 8 datagrams, no persistent cap.  Measured on the
+// config-2 batch (tools/kvariants.py xor_*): 16 lanes / nt / 8 workgroups per
+// CU 1.04 ms, default policy 0.81, 64 lanes x 2 pieces 0.67, 32 lanes x 4
+// pieces uncapped 0.59 ms = 5.0 TB/s read + write; masked atomicXor per word
+// for the edge pieces 1.73 ms.
+//
+// Key bytes come from LDS: four copies of the periodic key stream shifted by
+// 0..3 bytes, so the 16 key bytes of any phase m are four aligned dword reads
+// from copy m & 3.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_kernels.h"
+
+namespace lnl {
+
+namespace {
+
+constexpr int kThreads = 256;
+// build knobs (tools/kvariants.py): lanes per datagram (LNL_XOR_GROUP,
+// crc32c_kernels.h), pieces per lane in flight, nt (1) or default (0) policy
+// for the whole-piece loads and stores
+#ifndef LNL_XOR_UNROLL
+#define LNL_XOR_UNROLL 4
+#endif
+#ifndef LNL_XOR_NT
+#define LNL_XOR_NT 0
+#endif
+constexpr int kGroup = LNL_XOR_GROUP;
+constexpr int kUnroll = LNL_XOR_UNROLL;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(kThreads) void xor_layer_kernel(XorArgs a) {
+    // key stream copies: S_s[i] = key[(i + s) % K], i < K + 20 (bytes), s = 0..3
+    __shared__ uint32_t ks[4][(kXorMaxKey + 20 + 3) / 4];
+    const uint32_t K = a.key_len;
+    const uint32_t words = (K + 20 + 3) / 4;
+    for (uint32_t t = threadIdx.x; t < 4 * words; t += kThreads) {
+        const uint32_t s = t / words, w = t - s * words;
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; ++b) v |= (uint32_t)a.key[(4 * w + b + s) % K] << (8 * b);
+        ks[s][w] = v;
+    }
+    __syncthreads();
+
+    const uint32_t groups = gridDim.x * (kThreads / kGroup);
+    const uint32_t sub = threadIdx.x % kGroup;
+    const uint32_t adv = (16u * kGroup) % K;  // key phase advance between a lane's pieces
+    for (uint32_t d = blockIdx.x * (kThreads / kGroup) + threadIdx.x / kGroup; d < a.n; d += groups) {
+        uint64_t start;
+        uint32_t len;
+        if (a.off) {
+            start = a.off[d] - a.off0;
+            len = (uint32_t)(a.off[d + 1] - a.off[d]);
+        } else {
+            start = (uint64_t)d * a.stride;
+            len = a.len;
+        }
+        if (len == 0) continue;
+        const uint64_t p0 = (uint64_t)(uintptr_t)(a.base + start), p1 = p0 + len;  // datagram bytes
+        const uint64_t q0 = p0 & ~(uint64_t)15;
+        const uint32_t head = (uint32_t)(p0 - q0);                  // bytes of piece 0 before p0
+        const uint32_t pieces = (uint32_t)((p1 - q0 + 15) >> 4);
+        // key phase of this lane's first piece's byte 0 (datagram offset 16 sub - head >= -15)
+        uint32_t m = (16u * sub + 15u * K - head) % K;
+        // four pieces per lane in flight: loads first, then XOR and stores
+        for (uint32_t k0 = sub; k0 < pieces; k0 += kUnroll * kGroup) {
+            u32x4 v[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint32_t k = k0 + (uint32_t)u * kGroup;
+                const uint64_t q = q0 + 16u * (uint64_t)k;
+                if (k < pieces && q >= p0 && q + 16u <= p1) {
+#if LNL_XOR_NT
+                    v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>((uintptr_t)q));
+#else
+                    v[u] = *reinterpret_cast<const u32x4*>((uintptr_t)q);
+#endif
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint32_t k = k0 + (uint32_t)u * kGroup;
+                if (k >= pieces) break;
+                const uint64_t q = q0 + 16u * (uint64_t)k;
+                const uint32_t* kw = &ks[m & 3u][(m - (m & 3u)) >> 2];
+                const u32x4 key4 = {kw[0], kw[1], kw[2], kw[3]};
+                if (q >= p0 && q + 16u <= p1) {  // whole piece inside the datagram
+#if LNL_XOR_NT
+                    __builtin_nontemporal_store(v[u] ^ key4, reinterpret_cast<u32x4*>((uintptr_t)q));
+#else
+                    *reinterpret_cast<u32x4*>((uintptr_t)q) = v[u] ^ key4;
+#endif
+                } else {
+                    // first / last piece: its other bytes belong to neighbouring
+                    // datagrams, updated concurrently by other lanes with byte
+                    // stores of their own -- read the piece, store this
+                    // datagram's bytes one by one
+                    const u32x4 pv = *reinterpret_cast<const u32x4*>((uintptr_t)q);
+                    const u32x4 x = pv ^ key4;
+                    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+                    uint8_t* bp = reinterpret_cast<uint8_t*>((uintptr_t)q);
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const uint64_t at = q + (uint64_t)j;
+                        if (at >= p0 && at < p1) bp[j] = (uint8_t)(xw[j >> 2] >> (8 * (j & 3)));
+                    }
+                }
+                m += adv;
+                if (m >= K) m -= K;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_xor_layer(const XorArgs& a, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(xor_layer_kernel, dim3(grid), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace lnl

@@ -163,3 +163,12 @@ def dispatch(wire_list, status):
             out.append((i, pos, L))
             pos += L
     return out
+
+
+def xor_layer(data: np.ndarray, key: bytes) -> np.ndarray:
+    """Upstream LiteNetLib XorEncryptLayer on one datagram (restated; the C#
+    source is not available offline -- parity unpinned):
+    data[i] ^= key[i % len(key)], the phase restarting at each datagram."""
+    d = np.asarray(data, dtype=np.uint8)
+    k = np.frombuffer(key, np.uint8)
+    return d ^ np.resize(k, d.size) if d.size else d.copy()

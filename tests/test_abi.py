@@ -37,7 +37,7 @@ def test_header_declares_the_boundary():
               "lnl_crc32c_layer_outbound", "lnl_crc32c_layer_inbound", "lnl_crc32c_last_error",
               "lnl_crc32c_batch_host_multi", "lnl_packet_verify", "lnl_inbound_status",
               "lnl_inbound_filter_csr_dev", "lnl_inbound_filter_host", "lnl_ingress_recv_batch",
-              "lnl_dispatch_csr_dev"):
+              "lnl_dispatch_csr_dev", "lnl_xor_layer", "lnl_xor_layer_csr_dev", "lnl_xor_layer_fixed_dev"):
         assert s in syms
 
 
@@ -47,7 +47,7 @@ def test_library_exports_every_declared_symbol(pkg):
     exported = set(re.findall(r"\bT (lnl_\w+)", out))
     missing = [s for s in declared_symbols() if s not in exported]
     assert not missing, missing
-    assert pkg.lib().lnl_crc32c_abi_version() == 5
+    assert pkg.lib().lnl_crc32c_abi_version() == 6
 
 
 def test_cpu_crc_matches_oracle(pkg):

@@ -558,6 +558,47 @@ def test_dispatch_merged_containers(P, n):
     assert p2.cpu().numpy().tolist() == [e[0] for e in exp[:7]]
 
 
+@pytest.mark.parametrize("klen", [1, 3, 16, 37, 256])
+def test_xor_layer_csr(P, klen):
+    """XorEncryptLayer over a device CSR batch, in place: every datagram equals
+    the restatement (phase restarts per datagram); neighbouring datagrams that
+    share a 16-byte piece keep each other's bytes; twice = identity."""
+    rng = np.random.default_rng(1000 + klen)
+    key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
+    n = 20000
+    lens = rng.integers(0, 1433, n)
+    lens[rng.integers(0, n, 3000)] = rng.integers(0, 20, 3000)      # many datagrams inside one piece
+    lead = int(rng.integers(0, 16))
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(lead)
+    data = rng.integers(0, 256, int(off[-1]) + 21, dtype=np.uint8)
+    d = dev(data)
+    o = dev(off.view(np.int64), torch.int64)
+    P.xor_layer_csr(d, o, key)
+    got = d.cpu().numpy()
+    exp = data.copy()
+    for i in range(n):
+        a, b = int(off[i]), int(off[i + 1])
+        exp[a:b] = oracle.xor_layer(data[a:b], key)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"
+    P.xor_layer_csr(d, o, key)
+    assert np.array_equal(d.cpu().numpy(), data)
+
+
+@pytest.mark.parametrize("stride,length", [(1400, 1400), (1408, 1400), (64, 17), (1432, 1)])
+def test_xor_layer_fixed(P, stride, length):
+    rng = np.random.default_rng(stride + length)
+    key = b"LiteNetLib"
+    n = 5000
+    data = rng.integers(0, 256, n * stride + 16, dtype=np.uint8)
+    d = dev(data)
+    P.xor_layer_fixed(d, stride, length, n, key)
+    exp = data.copy()
+    for i in range(n):
+        exp[i * stride:i * stride + length] = oracle.xor_layer(data[i * stride:i * stride + length], key)
+    assert np.array_equal(d.cpu().numpy(), exp)
+
+
 def test_full_config2_bit_exact(P):
     # BASELINE config 2 at full size: 2^20 x 1400 B, every CRC compared
     n, L = 1 << 20, 1400

@@ -36,6 +36,18 @@ VARIANTS = {
     "csr_memonly": ("-DLNL_CSR_DIAG_MEMONLY", 1),   # uniform kernel, rows loaded and read only (wrong CRCs)
     "pair_edge_nt": ("-DLNL_PAIR_EDGE_AUX=2", 3),   # pair kernel: nt for the shared-line fetches too
     "pair_dflt": ("-DLNL_PAIR_AUX=0", 3),           # pair kernel: default policy for every fetch
+    "xor_dflt": "-DLNL_XOR_NT=0",                   # XOR layer: default policy loads / stores
+    "xor_g64": "-DLNL_XOR_GROUP=64",                # XOR layer: one datagram per wave
+    "xor_g64u2": "-DLNL_XOR_GROUP=64 -DLNL_XOR_UNROLL=2",
+    "xor_u1": "-DLNL_XOR_UNROLL=1",
+    "xor_g64u2d": "-DLNL_XOR_GROUP=64 -DLNL_XOR_UNROLL=2 -DLNL_XOR_NT=0",
+    "xor_g64u2d_nocap": "-DLNL_XOR_GROUP=64 -DLNL_XOR_UNROLL=2 -DLNL_XOR_NT=0 -DLNL_XOR_WG_PER_CU=0",
+    "xor_g32u4d_nocap": "-DLNL_XOR_GROUP=32 -DLNL_XOR_UNROLL=4 -DLNL_XOR_NT=0 -DLNL_XOR_WG_PER_CU=0",
+    "xor_g16u4d_nocap": "-DLNL_XOR_GROUP=16 -DLNL_XOR_UNROLL=4 -DLNL_XOR_NT=0 -DLNL_XOR_WG_PER_CU=0",
+    "xor_g64u2_nocap": "-DLNL_XOR_GROUP=64 -DLNL_XOR_UNROLL=2 -DLNL_XOR_WG_PER_CU=0",
+    "xor_g32u4_nocap": "-DLNL_XOR_GROUP=32 -DLNL_XOR_UNROLL=4 -DLNL_XOR_WG_PER_CU=0",
+    "xor_g32u4d_cap16": "-DLNL_XOR_GROUP=32 -DLNL_XOR_UNROLL=4 -DLNL_XOR_NT=0 -DLNL_XOR_WG_PER_CU=16",
+    "xor_g32u3d_nocap": "-DLNL_XOR_GROUP=32 -DLNL_XOR_UNROLL=3 -DLNL_XOR_NT=0 -DLNL_XOR_WG_PER_CU=0",
     "run_sc0": "-DLNL_RUN_AUX=1",
     "run_sc0nt": "-DLNL_RUN_AUX=3",
     "run_sc1": "-DLNL_RUN_AUX=16",
@@ -71,6 +83,8 @@ def run(names, rounds, workloads):
                                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         L.lnl_crc32c_batch_csr_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                ctypes.c_void_p, ctypes.c_void_p]
+        L.lnl_xor_layer_fixed_dev.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                              ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
         path = flags_path(VARIANTS[n])[1]
         if path is not None:
             L.lnl_crc32c_set_csr_path(path)
@@ -81,7 +95,16 @@ def run(names, rounds, workloads):
     results = {}
     for wl in workloads:
         s = torch.cuda.current_stream()
-        if wl[0] == "csr":  # ("csr", n, lmin, lmax): config-3-shaped CSR batch
+        if wl[0] == "xor":  # ("xor", n, len): XOR layer in place over n x len at stride len
+            _, n_pk, L_pk = wl
+            data = torch.randint(0, 256, (n_pk * L_pk,), dtype=torch.uint8, device=dev, generator=g)
+            algo = 2 * n_pk * L_pk
+            wkey = f"xor{n_pk}x{L_pk}"
+            key = b"LiteNetLibPP-bench-key"
+
+            def call(L):
+                L.lnl_xor_layer_fixed_dev(data.data_ptr(), L_pk, L_pk, n_pk, key, len(key), s.cuda_stream)
+        elif wl[0] == "csr":  # ("csr", n, lmin, lmax): config-3-shaped CSR batch
             _, n_pk, lmin, lmax = wl
             lens = torch.randint(lmin, lmax + 1, (n_pk,), device=dev, generator=g, dtype=torch.int64)
             off = torch.zeros(n_pk + 1, dtype=torch.int64, device=dev)
@@ -138,7 +161,7 @@ def main():
     if a.cmd == "build":
         build(names)
     else:
-        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.startswith("csr")
+        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w[:3] in ("csr", "xor")
               else tuple(int(v) for v in w.split(":")) for w in a.workloads.split(",")]
         res = run(names, a.rounds, wl)
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
