@@ -315,8 +315,7 @@ int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st)
         }
     }
     void* scratch = nullptr;
-    // counts + fill (kBucketCounterWords, a multiple of 16 bytes), then the descriptors
-    const size_t bytes = lnl::kBucketCounterWords * sizeof(uint32_t) + (size_t)a.n * sizeof(uint4);
+    const size_t bytes = lnl::bucket_scratch_words(a.n) * sizeof(uint32_t);
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
     if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
     lnl::BucketArgs b{};
@@ -325,15 +324,14 @@ int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st)
     b.off0 = a.off0;
     b.n = a.n;
     b.verify = mode == lnl::kModeVerify;
-    b.counts = (uint32_t*)scratch;
-    b.fill = b.counts + lnl::kCounterCopies * lnl::kBuckets;
-    b.desc = (uint4*)(b.counts + lnl::kBucketCounterWords);
+    lnl::bucket_layout(b, (uint32_t*)scratch);
     e = lnl::launch_csr_buckets(b, st);
     int rc = 0;
     if (e != hipSuccess) {
         rc = hip_fail(e, "bucket pre-pass launch");
     } else {
         a.desc = b.desc;
+        a.perm_n = b.ctl;  // null for the atomic layout (n descriptors)
         rc = launch(S, a, mode, st);
     }
     e = hipFreeAsync(scratch, st);
