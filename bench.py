@@ -49,9 +49,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["fixed", "csr", "xor"], default="fixed",
-                    help="fixed: config 2 (the headline); csr: config 3; xor: the XOR-encryption "
-                         "layer in place over the config-2 batch (SURVEY 8(f) item 4)")
+    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor"], default="fixed",
+                    help="fixed: config 2 (the headline); csr: config 3; filter: the batched inbound "
+                         "filter (CRC check + net_packet::verify) over the config-3 batch as wire "
+                         "datagrams; xor: the XOR-encryption layer in place over the config-2 batch")
     ap.add_argument("--packets", type=int, default=1 << 20, help="per GPU")
     ap.add_argument("--length", type=int, default=1400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -74,12 +75,15 @@ def make_workload(args, rank, world, device):
         L = args.length
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
         return dict(data=data, n=n, L=L, off=None, payload=n * L, algo=n * L + 4 * n)
-    # config 3: lengths 64 + U[0, 1337), packed CSR with int64 offsets
+    # config 3: lengths 64 + U[0, 1337), packed CSR with int64 offsets (filter: the
+    # same bytes read as wire datagrams, each ending in its 4-byte CRC field)
     lens = torch.randint(64, 1401, (n,), dtype=torch.int64, device=device, generator=g)
     off = torch.zeros(n + 1, dtype=torch.int64, device=device)
     off[1:] = torch.cumsum(lens, 0)
     total = int(off[-1].item())
     data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=device, generator=g)
+    if args.workload == "filter":  # status byte out instead of a CRC word
+        return dict(data=data, n=n, L=None, off=off, payload=total, algo=total + n + 8 * (n + 1), filter=True)
     return dict(data=data, n=n, L=None, off=off, payload=total, algo=total + 4 * n + 8 * (n + 1))
 
 
@@ -89,6 +93,8 @@ XOR_KEY = b"LiteNetLibPP-bench-key"
 def launch(P, w, out, stream):
     if w.get("xor"):
         P.xor_layer_fixed(w["data"], w["L"], w["L"], w["n"], XOR_KEY, stream=stream)
+    elif w.get("filter"):
+        P.inbound_filter(w["data"], w["off"], out=w["status"], stream=stream)
     elif w["off"] is None:
         P.batch_fixed(w["data"], w["L"], w["L"], w["n"], out=out, stream=stream)
     else:
@@ -178,6 +184,8 @@ def main():
 
     w = make_workload(args, rank, world, device)
     out = torch.empty(w["n"], dtype=torch.int32, device=device)
+    if w.get("filter"):
+        w["status"] = torch.empty(w["n"], dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
         launch(P, w, out, stream)
@@ -217,6 +225,7 @@ def main():
         line = {
             "metric": {"fixed": METRIC,
                        "csr": "CRC32C GB/s (device-resident) over 1M mixed-length (64-1400B) packets; bit-exact",
+                       "filter": "inbound filter GB/s (CRC check + verify, device-resident) over 1M mixed-length (64-1400B) datagrams",
                        "xor": "XOR-layer GB/s (device-resident, in place) over 1M x 1400B packets"}[args.workload],
             "value": round(value, 2),
             "unit": "GB/s",
@@ -232,6 +241,7 @@ def main():
             "config": {
                 "workload": {"fixed": "config2: 2^20 x 1400 B datagrams per GPU, fixed stride 1400, device-resident",
                              "csr": "config3: 2^20 mixed-length datagrams (64..1400 B uniform) per GPU, CSR int64 offsets",
+                             "filter": "config-3 batch as wire datagrams through lnl_inbound_filter_csr_dev",
                              "xor": "XOR layer over the config-2 batch, in place (22-byte key)"}[args.workload],
                 "packets_per_gpu": w["n"],
                 "payload_bytes_per_gpu": w["payload"],
@@ -251,7 +261,7 @@ def main():
         probe = hbm_probe_peak(w["data"], device)
         if probe:
             line["roofline"]["measured_stream_read_peak_gbs"] = round(probe, 1)
-        if world == 1 and not args.no_cpu_baseline and not w.get("xor"):
+        if world == 1 and not args.no_cpu_baseline and not (w.get("xor") or w.get("filter")):
             gpu_out = out.cpu().numpy().view(np.uint32)
             res, threads, desc, exact = cpu_baseline(w, gpu_out)
             line["cpu_baseline"] = {

@@ -202,14 +202,16 @@ def inbound_status(wire) -> int:
     return int(lib().lnl_inbound_status(addr, n))
 
 
-def inbound_filter(data, offsets, stream=None):
+def inbound_filter(data, offsets, out=None, stream=None):
     """Batched inbound filter on the GPU: status[i] of every wire datagram of a
     CSR batch (uint8: INBOUND_DROP_CRC / INBOUND_ACCEPT / INBOUND_MALFORMED)."""
     torch = _torch()
     _check_dev_u8(data, "data")
     _check_off(offsets, data)
     n = offsets.numel() - 1
-    status = torch.empty(max(n, 0), dtype=torch.uint8, device=data.device)
+    status = out if out is not None else torch.empty(max(n, 0), dtype=torch.uint8, device=data.device)
+    if status.dtype != torch.uint8 or status.numel() < max(n, 0) or status.device != data.device:
+        raise ValueError("out must be a uint8 tensor of n entries on the data's device")
     if n > 0:
         check(lib().lnl_inbound_filter_csr_dev(data.data_ptr(), offsets.data_ptr(), n, status.data_ptr(),
                                                _stream_handle(stream)), "lnl_inbound_filter_csr_dev")

@@ -21,8 +21,9 @@ sys.path.insert(0, os.path.join(ROOT, "litenetlibpp_amd", "tools"))
 from prof_summary import from_db, short  # noqa: E402
 
 # kernels of liblnl_crc32c.so (rocprofv3 names contain these)
-PRODUCT_KERNELS = ("crc32c_", "bucket_count", "bucket_scatter", "pair_count", "pair_scatter",
-                   "seg_prep", "seg_fixup", "verify_from_wire")
+PRODUCT_KERNELS = ("crc32c_", "bucket_count", "bucket_scatter", "bucket_hist", "bucket_scan", "bucket_place",
+                   "pair_count", "pair_scatter", "seg_prep", "seg_fixup", "verify_from_wire", "csr_plan",
+                   "dispatch_", "xor_layer")
 
 
 def main():
@@ -38,7 +39,7 @@ def main():
           "(kernel trace; then one PMC pass per counter group).\n"]
     # HBM bytes per API call: every product kernel the call launches (the CRC
     # kernel plus, for CSR, its bucket pre-pass), counter totals divided by the
-    # dispatch count of the dominant CRC kernel (the one with the most time)
+    # dispatch count of the dominant product kernel (the one with the most time)
     pmc_tot = {}
     kernels = set()
     trace_stats = None
@@ -56,7 +57,7 @@ def main():
                 kernels.add(short(name))
                 for cn, vals in cs.items():
                     pmc_tot[cn] = pmc_tot.get(cn, 0.0) + sum(vals)
-    crc = {n: d for n, d in trace_stats.items() if "crc32c" in n}
+    crc = {n: d for n, d in trace_stats.items() if any(k in n for k in PRODUCT_KERNELS)}
     dom = max(crc, key=lambda n: sum(crc[n]))
     crc_kernel = short(dom)
     calls = len(crc[dom])
