@@ -12,18 +12,13 @@
 // instead of an index plus two random offset reads -- so a wave's lanes need
 // the same number of rows.
 //
-// Two passes over the offsets (8 bytes per datagram each), both cheap next to
-// the payload: count per bucket (wave histograms in LDS, one global atomic
-// per workgroup and bucket), then scatter (the workgroup reserves a range per
-// bucket with one global atomic and places its datagrams with their LDS
-// ranks).  The global counters exist in kCounterCopies copies (workgroup w
-// uses copy w % kCounterCopies; each bucket's range is split into one
-// sub-range per copy), so no counter takes more than 64 of the 1024
-// workgroups' atomics -- with a single copy the serialized atomics made both
-// passes ~50 % slower.  Order within a bucket depends on atomic order; CRCs are written by
-// datagram index, so results do not.  Workgroups take 1024 datagrams each, so
-// a config-3 batch (2^20) launches 1024 of them: four per CU keep enough
-// offset loads in flight.
+// Three small launches over the offsets (8 bytes per datagram, read twice),
+// cheap next to the payload: a histogram per workgroup of 1024 datagrams, a
+// per-bucket exclusive scan over the workgroups, then the placement (scanned
+// base + LDS rank).  Buckets stay in datagram order and the layout is
+// deterministic; see LNL_BUCKET_LAYOUT below for the two measured
+// alternatives.  CRCs are written by datagram index, so results never depend
+// on the layout.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,6 +27,20 @@
 namespace lnl {
 
 namespace {
+
+// Descriptor layout (LNL_BUCKET_LAYOUT):
+//   0 atomic    bucket after bucket, ranks from global atomics (16 counter
+//               copies, so a bucket is 16 interleaved runs), counters memset
+//   1 interleave position-ordered buckets, batches interleaved by progress so
+//               that neighbouring datagrams are processed together -- parity
+//               clean but slower: 0.230 ms per config-3 batch (the batch kernel
+//               itself 155 -> 190 us), placing the descriptors 25 us
+//   2 ordered   (default) position-ordered buckets, bucket after bucket: ranks
+//               from per-workgroup histograms and a per-bucket scan, no global
+//               atomics, no memset, deterministic; as fast as 0 (0.174-0.177 ms)
+#ifndef LNL_BUCKET_LAYOUT
+#define LNL_BUCKET_LAYOUT 2
+#endif
 
 constexpr int kThreads = 256;
 constexpr int kPerThread = 16;                    // pair count pass
@@ -132,19 +141,17 @@ __global__ __launch_bounds__(kThreads) void bucket_scatter_kernel(BucketArgs a) 
     }
 }
 
-// ---- interleaved, position-ordered layout (LNL_BUCKET_INTERLEAVE=1; experiment) ---
+// ---- position-ordered layouts (LNL_BUCKET_LAYOUT 1 and 2) ---------------------
 //
-// The atomic layout lists bucket after bucket, so datagram i and its
-// neighbour i+1 (usually in another bucket) are processed far apart in time
-// and the line they share is fetched from HBM twice.  This layout keeps every
-// bucket in datagram order (ranks from per-workgroup histograms and a
-// per-bucket scan -- no global atomics, no counter memset) and interleaves
-// the buckets' batches by progress: batch j of bucket k (nb_k batches) sits at
-// "time" (j + 1/2) / nb_k, and batches are laid out in that order (ties by
-// bucket).  At any moment the chip then works on a narrow window of the
-// buffer in every bucket at once, so the second fetch of a shared line finds
-// it in L2 / the Infinity Cache.  Each bucket's last batch is padded with idle
-// entries (index n), so batches never mix buckets.
+// Every bucket is kept in datagram order: ranks from per-workgroup histograms
+// and a per-bucket scan (no global atomics, no counter memset).  Layout 2 lists
+// bucket after bucket.  Layout 1 also interleaves the buckets' batches by
+// progress -- batch j of bucket k (nb_k batches) sits at "time" (j + 1/2) / nb_k,
+// ties by bucket -- so that the chip works on a narrow window of the buffer in
+// every bucket at once and the second fetch of a line two neighbouring
+// datagrams share could hit in L2 / the Infinity Cache; measured slower.
+// Each bucket's last batch is padded with idle entries (index n), so batches
+// never mix buckets.
 
 // batches of bucket k before time (2j+1) / (2 nb) in the interleaved order,
 // counting bucket k2 (nb2 batches); ties go to the lower bucket
@@ -160,6 +167,10 @@ __device__ inline uint32_t batches_before(uint32_t j, uint32_t nb, uint32_t k, u
 
 __device__ inline uint32_t merged_batch(uint32_t k, uint32_t j, const uint32_t* nbs) {
     uint32_t b = 0;
+#if LNL_BUCKET_LAYOUT == 2  // ordered: bucket after bucket
+    for (uint32_t k2 = 0; k2 < k; ++k2) b += nbs[k2];
+    return b + j;
+#endif
     for (uint32_t k2 = 0; k2 < (uint32_t)kBuckets; ++k2) b += batches_before(j, nbs[k], k, nbs[k2], k2);
     return b;
 }
@@ -433,26 +444,19 @@ hipError_t launch_pair_prep(const PairPrepArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// The interleaved layout is an experiment, off by default: it measured
-// 0.231 ms per config-3 batch against 0.175 for the atomic layout -- the
-// batch kernel itself went from 155 to 190 us (the shared-line reuse did not
-// pay for what the position-ordered, bucket-interleaved batches cost it), and
-// placing the descriptors took 25 us.
-#ifndef LNL_BUCKET_INTERLEAVE
-#define LNL_BUCKET_INTERLEAVE 0
-#endif
+
 
 size_t bucket_scratch_words(uint32_t n) {
     const size_t groups = ((size_t)n + kBucketPerBlock - 1) / kBucketPerBlock;
     // hist + pbase + tot + ctl (rounded to 16 B), then n descriptors + padding of every bucket
-    const size_t head = LNL_BUCKET_INTERLEAVE ? 2 * groups * kBuckets + kBuckets + 4 : kBucketCounterWords;
+    const size_t head = LNL_BUCKET_LAYOUT ? 2 * groups * kBuckets + kBuckets + 4 : kBucketCounterWords;
     return (head + 3) / 4 * 4 + 4 * ((size_t)n + 64u * kBuckets);
 }
 
 void bucket_layout(BucketArgs& a, uint32_t* w) {
     const size_t groups = ((size_t)a.n + kBucketPerBlock - 1) / kBucketPerBlock;
     size_t head;
-    if (LNL_BUCKET_INTERLEAVE) {
+    if (LNL_BUCKET_LAYOUT) {
         a.hist = w;
         a.pbase = a.hist + groups * kBuckets;
         a.tot = a.pbase + groups * kBuckets;
@@ -470,7 +474,7 @@ void bucket_layout(BucketArgs& a, uint32_t* w) {
 
 hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream) {
     const uint32_t groups = (a.n + kBucketPerBlock - 1) / kBucketPerBlock;
-    if (LNL_BUCKET_INTERLEAVE) {
+    if (LNL_BUCKET_LAYOUT) {
         hipLaunchKernelGGL(bucket_hist_kernel, dim3(groups), dim3(kThreads), 0, stream, a);
         hipLaunchKernelGGL(bucket_scan_kernel, dim3(kBuckets), dim3(kThreads), 0, stream, a, groups);
         hipLaunchKernelGGL(bucket_place_kernel, dim3(groups), dim3(kThreads), 0, stream, a);

@@ -63,14 +63,14 @@ struct BucketArgs {
     uint64_t off0;
     uint32_t n;
     uint32_t verify;  // verify mode: the CRC covers all but the last 4 bytes
-    // interleaved layout (LNL_BUCKET_INTERLEAVE, the default): per-workgroup
-    // histograms, their per-bucket prefix, bucket totals, and the descriptor
-    // count the batch kernel reads as perm_n
+    // position-ordered layouts (LNL_BUCKET_LAYOUT 1, 2 -- 2 is the default):
+    // per-workgroup histograms, their per-bucket prefix, bucket totals, and
+    // the descriptor count the batch kernel reads as perm_n
     uint32_t* hist;   // groups x kBuckets
     uint32_t* pbase;  // groups x kBuckets
     uint32_t* tot;    // kBuckets
     uint32_t* ctl;    // [0]: descriptors incl. idle padding (64 x batches)
-    // atomic layout (LNL_BUCKET_INTERLEAVE=0)
+    // atomic layout (LNL_BUCKET_LAYOUT 0)
     uint32_t* counts;
     uint32_t* fill;   // counts + kCounterCopies * kBuckets
     uint4* desc;      // BatchArgs::desc layout, 16-byte aligned

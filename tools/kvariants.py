@@ -36,7 +36,8 @@ VARIANTS = {
     "csr_memonly": ("-DLNL_CSR_DIAG_MEMONLY", 1),   # uniform kernel, rows loaded and read only (wrong CRCs)
     "pair_edge_nt": ("-DLNL_PAIR_EDGE_AUX=2", 3),   # pair kernel: nt for the shared-line fetches too
     "pair_dflt": ("-DLNL_PAIR_AUX=0", 3),           # pair kernel: default policy for every fetch
-    "bucket_interleave": "-DLNL_BUCKET_INTERLEAVE=1",  # CSR: position-ordered buckets, batches interleaved by progress
+    "bucket_atomic": "-DLNL_BUCKET_LAYOUT=0",       # CSR: atomic ranks, bucket after bucket (16 runs per bucket)
+    "bucket_interleave": "-DLNL_BUCKET_LAYOUT=1",   # CSR: position-ordered buckets, batches interleaved by progress
     "xor_dflt": "-DLNL_XOR_NT=0",                   # XOR layer: default policy loads / stores
     "xor_g64": "-DLNL_XOR_GROUP=64",                # XOR layer: one datagram per wave
     "xor_g64u2": "-DLNL_XOR_GROUP=64 -DLNL_XOR_UNROLL=2",
