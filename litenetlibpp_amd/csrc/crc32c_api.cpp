@@ -131,15 +131,10 @@ int current_device(DeviceState** S) {
     return device_state(dev, S);
 }
 
-int grid_for(const DeviceState& S, uint32_t n) {
-    const uint32_t waves = (n + 63u) / 64u;
-    const uint32_t wgs = (waves + (lnl::kBlockThreads / 64) - 1) / (lnl::kBlockThreads / 64);
-    const uint32_t cap = (uint32_t)S.cus * (uint32_t)(lnl::kWavesPerCU / (lnl::kBlockThreads / 64));
-    return (int)std::max(1u, std::min(wgs, cap));
-}
-
-int grid_for_waves(const DeviceState& S, uint32_t waves) {
-    const uint32_t per_wg = lnl::kBlockThreads / 64;
+// persistent grid of `threads`-thread workgroups for `waves` waves of work
+// (at most kWavesPerCU resident waves per CU)
+int grid_for_waves(const DeviceState& S, uint32_t waves, int threads = lnl::kBlockThreads) {
+    const uint32_t per_wg = (uint32_t)threads / 64;
     const uint32_t wgs = (waves + per_wg - 1) / per_wg;
     const uint32_t cap = (uint32_t)S.cus * (uint32_t)(lnl::kWavesPerCU / per_wg);
     return (int)std::max(1u, std::min(wgs, cap));
@@ -148,7 +143,7 @@ int grid_for_waves(const DeviceState& S, uint32_t waves) {
 int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
     a.dummy = S.dummy;
     a.fold = S.fold;
-    hipError_t e = lnl::launch_crc32c_batch(a, mode, grid_for(S, a.n), st);
+    hipError_t e = lnl::launch_crc32c_batch(a, mode, grid_for_waves(S, (a.n + 63u) / 64u), st);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     return 0;
 }
@@ -289,7 +284,7 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
     // batches <= n / 64 + one partial batch per key
     const uint32_t waves_max = a.n / 64u + lnl::kBuckets;
     int rc = 0;
-    e = lnl::launch_csr_uniform(p, c, grid_for_waves(S, waves_max), st);
+    e = lnl::launch_csr_uniform(p, c, grid_for_waves(S, waves_max, 512), st);  // kThreads of crc32c_csr.hip
     if (e != hipSuccess) rc = hip_fail(e, "CSR uniform launch");
     if (rc == 0) {
         lnl::BatchArgs o = a;
