@@ -29,7 +29,7 @@ PRODUCT_KERNELS = ("crc32c_", "bucket_count", "bucket_scatter", "bucket_hist", "
 def main():
     tag, wl = sys.argv[1], sys.argv[2]
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{wl}")
-    dst = os.path.join(ROOT, "profiles")
+    dst = os.environ.get("PROFILES_DIR", os.path.join(ROOT, "profiles"))
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "t_kernel_stats.csv"),
                 os.path.join(dst, f"{tag}_{wl}_kernel_stats.csv"))
