@@ -84,6 +84,7 @@ struct Batch {
     // compute lane
     uint32_t p;      // datagram index (>= n: idle lane)
     uint32_t len;    // bytes covered by the CRC
+    const uint8_t* dptr;  // the datagram's first byte (verify mode: header byte, trailing CRC at dptr + len)
     uint32_t T;      // lines the datagram touches (0: idle)
     uint32_t first;  // first real row of this lane (rows before it are virtual)
     uint32_t pad;    // bytes of the first line before the datagram
@@ -157,6 +158,7 @@ __device__ LNL_INLINE void make_batch(const BatchArgs& a, uint32_t b, uint32_t n
     const uint64_t abs1 = abs0 + len - 1u;  // last byte (unused when len == 0)
     const uint32_t idle = len == 0u ? 1u : 0u;
     B.len = len;
+    B.dptr = a.base + start;
     B.T = idle ? 0u : (uint32_t)((abs1 >> 7) - (abs0 >> 7)) + 1u;
     B.pad = (uint32_t)abs0 & 127u;
     B.e = 127u - ((uint32_t)abs1 & 127u);
@@ -232,17 +234,17 @@ template <int kMode>
 __device__ LNL_INLINE void store_result(const BatchArgs& a, const Batch& B, uint32_t crc) {
     if (B.p >= a.n) return;
     if constexpr (kMode == kModeVerify) {
-        const uint64_t e = a.off[B.p + 1];
-        const uint32_t total = (uint32_t)(e - a.off[B.p]);
+        // B.len = total - 4 for datagrams of >= 5 bytes, else 0 (lane_extent,
+        // bucket_of): the trailing CRC follows the covered bytes
         uint32_t ok = 0;
-        if (total >= 5u) {
-            const uint8_t* tail = a.base + (e - a.off0) - 4;
+        if (B.len) {
+            const uint8_t* tail = B.dptr + B.len;
             const uint32_t stored = (uint32_t)tail[0] | ((uint32_t)tail[1] << 8) |
                                     ((uint32_t)tail[2] << 16) | ((uint32_t)tail[3] << 24);
             ok = stored == crc;
             // inbound filter: the CRC layer passed it, now net_packet::verify()
             // on the stripped packet (net_manager.cpp:343)
-            if (ok && a.filter) ok = lnl_packet_verify_hdr(a.base[a.off[B.p] - a.off0], total - 4u) ? 1u : 2u;
+            if (ok && a.filter) ok = lnl_packet_verify_hdr(B.dptr[0], B.len) ? 1u : 2u;
         }
         a.ok[B.p] = (uint8_t)ok;
         if (a.out) a.out[B.p] = crc;
