@@ -49,10 +49,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor"], default="fixed",
+    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "dispatch"], default="fixed",
                     help="fixed: config 2 (the headline); csr: config 3; filter: the batched inbound "
                          "filter (CRC check + net_packet::verify) over the config-3 batch as wire "
-                         "datagrams; xor: the XOR-encryption layer in place over the config-2 batch")
+                         "datagrams; xor: the XOR-encryption layer in place over the config-2 batch; "
+                         "dispatch: lnl_dispatch_csr_dev over accepted MERGED containers of 256-B "
+                         "messages (the config-1 traffic shape)")
     ap.add_argument("--packets", type=int, default=1 << 20, help="per GPU")
     ap.add_argument("--length", type=int, default=1400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -71,6 +73,8 @@ def make_workload(args, rank, world, device):
         L = args.length
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
         return dict(data=data, n=n, L=L, off=None, payload=n * L, algo=2 * n * L, xor=True)
+    if args.workload == "dispatch":
+        return make_dispatch_workload(n, device, g)
     if args.workload == "fixed":
         L = args.length
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
@@ -88,10 +92,49 @@ def make_workload(args, rank, world, device):
 
 
 XOR_KEY = b"LiteNetLibPP-bench-key"
+DISPATCH_SUBS = 5          # 256-B user messages per MERGED container (config 1's payload size)
+DISPATCH_SUB = 2 + 1 + 256  # [u16 LE size][UNRELIABLE header byte][256 B payload]
+DISPATCH_STRIDE = 1 + DISPATCH_SUBS * DISPATCH_SUB + 4
+
+
+def make_dispatch_workload(n, device, g):
+    """MERGED containers as net_peer::send_merged lays them out
+    (/root/reference/src/lnl/net_peer.cpp:446-486), each carrying five 257-B
+    UNRELIABLE packets and ending in its CRC-32C field; filtered once
+    (untimed) so every status is LNL_INBOUND_ACCEPT."""
+    import litenetlibpp_amd as P
+    S = DISPATCH_STRIDE
+    data = torch.randint(0, 256, (n * S,), dtype=torch.uint8, device=device, generator=g)
+    d = data.view(n, S)
+    d[:, 0] = 0x0C
+    for j in range(DISPATCH_SUBS):
+        b = 1 + j * DISPATCH_SUB
+        d[:, b] = (DISPATCH_SUB - 2) & 0xFF
+        d[:, b + 1] = (DISPATCH_SUB - 2) >> 8
+        d[:, b + 2] = 0x00
+    crc = P.batch_fixed(data, S, S - 4, n)
+    d[:, S - 4:] = crc.view(torch.uint8).view(n, 4)
+    off = torch.arange(0, (n + 1) * S, S, dtype=torch.int64, device=device)
+    status = P.inbound_filter(data, off)
+    assert bool((status == 1).all()), "dispatch workload: filter rejected a container"
+    k = n * DISPATCH_SUBS
+    # algorithmic bytes: offset, status and container header byte per datagram;
+    # u16 size + header byte read and {start, len, parent} (16 B) written per packet
+    return dict(data=data, n=n, L=None, off=off, payload=n * S, algo=n * (8 + 1 + 1) + k * (3 + 16),
+                dispatch=True, status=status, pkts=k,
+                pkt_start=torch.empty(k, dtype=torch.int64, device=device),
+                pkt_len=torch.empty(k, dtype=torch.int32, device=device),
+                pkt_parent=torch.empty(k, dtype=torch.int32, device=device),
+                total=torch.zeros(1, dtype=torch.int32, device=device))
 
 
 def launch(P, w, out, stream):
-    if w.get("xor"):
+    if w.get("dispatch"):
+        P._lib.check(P.lib().lnl_dispatch_csr_dev(
+            w["data"].data_ptr(), w["off"].data_ptr(), w["n"], w["status"].data_ptr(),
+            w["pkt_start"].data_ptr(), w["pkt_len"].data_ptr(), w["pkt_parent"].data_ptr(), w["pkts"],
+            w["total"].data_ptr(), stream.cuda_stream), "lnl_dispatch_csr_dev")
+    elif w.get("xor"):
         P.xor_layer_fixed(w["data"], w["L"], w["L"], w["n"], XOR_KEY, stream=stream)
     elif w.get("filter"):
         P.inbound_filter(w["data"], w["off"], out=w["status"], stream=stream)
@@ -184,7 +227,7 @@ def main():
 
     w = make_workload(args, rank, world, device)
     out = torch.empty(w["n"], dtype=torch.int32, device=device)
-    if w.get("filter"):
+    if w.get("filter") and "status" not in w:
         w["status"] = torch.empty(w["n"], dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
@@ -226,7 +269,8 @@ def main():
             "metric": {"fixed": METRIC,
                        "csr": "CRC32C GB/s (device-resident) over 1M mixed-length (64-1400B) packets; bit-exact",
                        "filter": "inbound filter GB/s (CRC check + verify, device-resident) over 1M mixed-length (64-1400B) datagrams",
-                       "xor": "XOR-layer GB/s (device-resident, in place) over 1M x 1400B packets"}[args.workload],
+                       "xor": "XOR-layer GB/s (device-resident, in place) over 1M x 1400B packets",
+                       "dispatch": "dispatch GB/s (MERGED containers cut on device) over 1M x 1300B datagrams"}[args.workload],
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -242,7 +286,8 @@ def main():
                 "workload": {"fixed": "config2: 2^20 x 1400 B datagrams per GPU, fixed stride 1400, device-resident",
                              "csr": "config3: 2^20 mixed-length datagrams (64..1400 B uniform) per GPU, CSR int64 offsets",
                              "filter": "config-3 batch as wire datagrams through lnl_inbound_filter_csr_dev",
-                             "xor": "XOR layer over the config-2 batch, in place (22-byte key)"}[args.workload],
+                             "xor": "XOR layer over the config-2 batch, in place (22-byte key)",
+                             "dispatch": "2^20 accepted MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire), lnl_dispatch_csr_dev"}[args.workload],
                 "packets_per_gpu": w["n"],
                 "payload_bytes_per_gpu": w["payload"],
                 "parallelism": f"shard{world} (contiguous packet ranges, no data-path collectives)",
@@ -261,7 +306,7 @@ def main():
         probe = hbm_probe_peak(w["data"], device)
         if probe:
             line["roofline"]["measured_stream_read_peak_gbs"] = round(probe, 1)
-        if world == 1 and not args.no_cpu_baseline and not (w.get("xor") or w.get("filter")):
+        if world == 1 and not args.no_cpu_baseline and not (w.get("xor") or w.get("filter") or w.get("dispatch")):
             gpu_out = out.cpu().numpy().view(np.uint32)
             res, threads, desc, exact = cpu_baseline(w, gpu_out)
             line["cpu_baseline"] = {

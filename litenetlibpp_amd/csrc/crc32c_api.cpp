@@ -619,7 +619,7 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     if (int rc = current_device(&S)) return rc;
     const size_t scan_bytes = lnl::dispatch_scan_bytes(n);
     void* scratch = nullptr;
-    const size_t bytes = 2 * (size_t)n * 4 + scan_bytes + 256;
+    const size_t bytes = (2 + (size_t)lnl::kDispatchRec) * n * 4 + scan_bytes + 256;
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
     if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
     lnl::DispatchArgs a{};
@@ -629,12 +629,13 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     a.status = d_status;
     a.counts = (uint32_t*)scratch;
     a.first = a.counts + n;
+    a.rec = a.first + n;
     a.pkt_start = d_pkt_start;
     a.pkt_len = d_pkt_len;
     a.pkt_parent = d_pkt_parent;
     a.cap = cap;
     a.total = d_total;
-    void* tmp = (void*)(((uintptr_t)(a.first + n) + 255) & ~(uintptr_t)255);
+    void* tmp = (void*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);
     int rc = 0;
     e = lnl::launch_dispatch(a, tmp, scan_bytes, st);
     if (e != hipSuccess) rc = hip_fail(e, "dispatch launch");

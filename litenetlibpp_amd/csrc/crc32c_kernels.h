@@ -212,12 +212,14 @@ struct DispatchArgs {
     const uint8_t* status;  // lnl_inbound_filter output
     uint32_t* counts;       // n (scratch)
     uint32_t* first;        // n (scratch): exclusive scan of counts
+    uint32_t* rec;          // kDispatchRec * n (scratch): (pos << 16 | len), slot-major
     uint64_t* pkt_start;    // cap: packet start relative to base
     uint32_t* pkt_len;      // cap
     uint32_t* pkt_parent;   // cap: datagram index
     uint32_t cap;
     uint32_t* total;        // device: packets delivered (may exceed cap)
 };
+constexpr uint32_t kDispatchRec = 8;  // packets per datagram kept from the counting walk
 size_t dispatch_scan_bytes(uint32_t n);
 hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
 

@@ -25,8 +25,11 @@
 // A nested container is delivered as one packet (the reference's
 // process_packet would cut it again); send_merged never nests.
 //
-// Two launches around a device-wide exclusive scan (hipCUB): count the packets
-// of every datagram, then emit them in datagram order.
+// Two launches around a device-wide exclusive scan (hipCUB): walk and count
+// the packets of every datagram (recording the first kDispatchRec), then emit
+// them in datagram order from the records.  A walk step is one dependent
+// round trip to a random 64-B sector, so walking each container once (not
+// once per pass) halves the latency-bound part of the call.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -40,51 +43,89 @@ namespace {
 
 constexpr uint32_t kMergedProperty = 12;  // PACKET_PROPERTY::MERGED, net_enums.h:60
 
+// Bytes q[0..2] (u16 LE size, then the packet's header byte) with two aligned
+// dword loads instead of three byte loads.  Safe whenever q[0..1] lie inside
+// the datagram: the walk only reads at pos with pos + 2 <= size, and the wire
+// datagram carries 4 more CRC bytes, so both dwords hold at least one byte of
+// the batch and never touch another page.
+__device__ inline uint32_t load3(const uint8_t* q) {
+    const uintptr_t a = (uintptr_t)q;
+    const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint64_t v = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    return (uint32_t)(v >> ((a & 3u) * 8u));
+}
+
 // Walk datagram i; for each delivered packet call emit(start, len) (start
-// relative to base).  Returns the number of packets.
+// relative to the datagram).  Returns the number of packets.
 template <typename F>
-__device__ inline uint32_t walk(const DispatchArgs& a, uint32_t i, F&& emit) {
-    if (a.status[i] != 1u) return 0;  // LNL_INBOUND_ACCEPT only
-    const uint64_t s = a.off[i] - a.off0;
-    const uint32_t size = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;  // CRC stripped
+__device__ inline uint32_t walk(const DispatchArgs& a, uint64_t s, uint32_t size, F&& emit) {
     const uint8_t* p = a.base + s;
     if ((p[0] & 0x1Fu) != kMergedProperty) {
-        emit(s, size);
+        emit(0u, size);
         return 1;
     }
     uint32_t pos = 1, c = 0;
     while (pos < size) {
         if (pos + 2u > size) break;
-        const uint32_t L = (uint32_t)p[pos] | ((uint32_t)p[pos + 1] << 8);
+        const uint32_t v = load3(p + pos);
+        const uint32_t L = v & 0xFFFFu;
         pos += 2;
         if (L > size - pos) break;
-        if (L == 0u || !lnl_packet_verify_hdr(p[pos], L)) break;
-        emit(s + pos, L);
+        if (L == 0u || !lnl_packet_verify_hdr((uint8_t)(v >> 16), L)) break;
+        emit(pos, L);
         pos += L;
         ++c;
     }
     return c;
 }
 
+// Pass 1: walk every accepted datagram once; count its packets and keep the
+// first kDispatchRec as (pos << 16 | len) records, slot-major so a wave's
+// stores are coalesced.
 __global__ __launch_bounds__(256) void dispatch_count_kernel(DispatchArgs a) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= a.n) return;
-    a.counts[i] = walk(a, i, [](uint64_t, uint32_t) {});
+    uint32_t c = 0;
+    if (a.status[i] == 1u) {  // LNL_INBOUND_ACCEPT only
+        const uint64_t s = a.off[i] - a.off0;
+        const uint32_t size = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;  // CRC stripped
+        uint32_t k = 0;
+        c = walk(a, s, size, [&](uint32_t pos, uint32_t len) {
+            if (k < kDispatchRec) a.rec[(size_t)k * a.n + i] = (pos << 16) | len;
+            ++k;
+        });
+    }
+    a.counts[i] = c;
 }
 
+// Pass 2: datagram i's packets go to [first[i], first[i] + counts[i]).  Up
+// to kDispatchRec of them come from pass 1's records; longer containers are
+// walked again.
 __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= a.n) return;
-    uint32_t k = a.first[i];
-    const uint32_t c = walk(a, i, [&](uint64_t start, uint32_t len) {
-        if (k < a.cap) {
-            a.pkt_start[k] = start;
-            a.pkt_len[k] = len;
-            a.pkt_parent[k] = i;
+    const uint32_t c = a.counts[i];
+    const uint32_t f = a.first[i];
+    if (i + 1u == a.n) *a.total = f + c;
+    if (c == 0u || f >= a.cap) return;
+    const uint64_t s = a.off[i] - a.off0;
+    const uint32_t size = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
+    auto put = [&](uint32_t k, uint32_t pos, uint32_t len) {
+        if (f + k < a.cap) {
+            a.pkt_start[f + k] = s + pos;
+            a.pkt_len[f + k] = len;
+            a.pkt_parent[f + k] = i;
         }
-        ++k;
-    });
-    if (i + 1u == a.n) *a.total = a.first[i] + c;
+    };
+    if (c <= kDispatchRec && size < 65536u) {  // records hold 16-bit positions
+        for (uint32_t k = 0; k < c; ++k) {
+            const uint32_t r = a.rec[(size_t)k * a.n + i];
+            put(k, r >> 16, r & 0xFFFFu);
+        }
+    } else {
+        uint32_t k = 0;
+        walk(a, s, size, [&](uint32_t pos, uint32_t len) { put(k++, pos, len); });
+    }
 }
 
 }  // namespace

@@ -558,6 +558,31 @@ def test_dispatch_merged_containers(P, n):
     assert p2.cpu().numpy().tolist() == [e[0] for e in exp[:7]]
 
 
+def test_dispatch_records_and_rewalk(P):
+    """The emit pass's two sources: containers of <= 8 packets come from the
+    counting walk's records, longer ones and datagrams of >= 64 KiB (16-bit
+    record positions) are walked again; all in datagram order."""
+    rng = np.random.default_rng(77)
+    layer = P.Crc32cLayer()
+    sub = lambda m: bytes([0x00]) + rng.integers(0, 256, m - 1, dtype=np.uint8).tobytes()
+    bodies = [_merged(rng, [sub(30000) for _ in range(3)], "ok"),      # 90 KB, 3 packets
+              _merged(rng, [sub(20) for _ in range(8)], "ok"),         # exactly 8 records
+              _merged(rng, [sub(20) for _ in range(9)], "ok"),         # one more: re-walk
+              _merged(rng, [sub(7) for _ in range(400)], "ok"),
+              bytes([0x01]) + sub(70000)]                              # plain, >= 64 KiB
+    wires = [bytes(layer.process_outbound(b)) for b in bodies] * 50
+    off = np.concatenate([[0], np.cumsum([len(w) for w in wires])]).astype(np.uint64)
+    blob = np.frombuffer(b"".join(wires), np.uint8)
+    d, o = dev(blob), dev(off.view(np.int64), torch.int64)
+    status = P.inbound_filter(d, o)
+    start, length, parent = P.dispatch(d, o, status)
+    exp = oracle.dispatch([np.frombuffer(w, np.uint8) for w in wires], status.cpu().numpy())
+    got = list(zip(parent.cpu().numpy().tolist(),
+                   (start.cpu().numpy() - off[parent.cpu().numpy()].astype(np.int64)).tolist(),
+                   length.cpu().numpy().tolist()))
+    assert got == exp and len(exp) == 50 * (3 + 8 + 9 + 400 + 1)
+
+
 @pytest.mark.parametrize("klen", [1, 3, 16, 37, 256])
 def test_xor_layer_csr(P, klen):
     """XorEncryptLayer over a device CSR batch, in place: every datagram equals
