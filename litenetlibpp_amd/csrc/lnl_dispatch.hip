@@ -98,18 +98,59 @@ __global__ __launch_bounds__(256) void dispatch_count_kernel(DispatchArgs a) {
     a.counts[i] = c;
 }
 
-// Pass 2: datagram i's packets go to [first[i], first[i] + counts[i]).  Up
-// to kDispatchRec of them come from pass 1's records; longer containers are
-// walked again.
+// Pass 2: datagram i's packets go to [first[i], first[i] + counts[i]).  A
+// wave owns 64 consecutive datagrams, whose packets form one contiguous range
+// of the output.  Datagrams whose packets all sit in pass 1's records (at most
+// kDispatchRec, positions < 64 KiB) are written cooperatively: lane l takes
+// packet F0 + l + 64t, finds its datagram by binary search over the wave's
+// `first` values in LDS, and the stores of consecutive lanes are consecutive.
+// Longer containers are walked again by their own lane.
+constexpr uint32_t kEmitMaxSteps = 16;  // cooperative only while the range is <= 16 x 64 packets
+
 __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= a.n) return;
-    const uint32_t c = a.counts[i];
-    const uint32_t f = a.first[i];
-    if (i + 1u == a.n) *a.total = f + c;
-    if (c == 0u || f >= a.cap) return;
-    const uint64_t s = a.off[i] - a.off0;
-    const uint32_t size = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
+    __shared__ uint32_t s_first[4][65];
+    __shared__ uint32_t s_fast[4][64];
+    __shared__ uint64_t s_start[4][64];
+    __shared__ uint32_t s_rec[4][kDispatchRec][64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t i0 = blockIdx.x * 256u + w * 64u;
+    const uint32_t i = i0 + lane;
+    uint32_t c = 0, f = 0, size = 0;
+    uint64_t s = 0;
+    if (i < a.n) {
+        c = a.counts[i];
+        f = a.first[i];
+        if (i + 1u == a.n) *a.total = f + c;
+        s = a.off[i] - a.off0;
+        if (c) size = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
+    } else if (i0 < a.n) {
+        f = a.first[a.n - 1] + a.counts[a.n - 1];  // past the end: empty, first = total
+    }
+    const bool fast = c <= kDispatchRec && size < 65536u;
+    s_first[w][lane] = f;
+    if (lane == 63u) s_first[w][64] = f + c;
+    s_fast[w][lane] = fast;
+    s_start[w][lane] = s;
+    for (uint32_t k = 0; k < kDispatchRec; ++k)
+        if (fast && k < c) s_rec[w][k][lane] = a.rec[(size_t)k * a.n + i];
+    __syncthreads();
+    if (i0 >= a.n) return;
+    const uint32_t F0 = s_first[w][0], F1 = s_first[w][64];
+    const bool coop = F1 - F0 <= kEmitMaxSteps * 64u;
+    if (coop) {
+        const uint32_t end = F1 < a.cap ? F1 : a.cap;
+        for (uint32_t j = F0 + lane; j < end; j += 64u) {
+            uint32_t lo = 0;  // last datagram d of the wave with first[d] <= j
+            for (uint32_t step = 32; step; step >>= 1)
+                if (s_first[w][lo + step] <= j && lo + step < 64u) lo += step;
+            if (!s_fast[w][lo]) continue;
+            const uint32_t r = s_rec[w][j - s_first[w][lo]][lo];
+            a.pkt_start[j] = s_start[w][lo] + (r >> 16);
+            a.pkt_len[j] = r & 0xFFFFu;
+            a.pkt_parent[j] = i0 + lo;
+        }
+    }
+    if (c == 0u || f >= a.cap || (coop && fast)) return;
     auto put = [&](uint32_t k, uint32_t pos, uint32_t len) {
         if (f + k < a.cap) {
             a.pkt_start[f + k] = s + pos;
@@ -117,9 +158,9 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
             a.pkt_parent[f + k] = i;
         }
     };
-    if (c <= kDispatchRec && size < 65536u) {  // records hold 16-bit positions
+    if (fast) {
         for (uint32_t k = 0; k < c; ++k) {
-            const uint32_t r = a.rec[(size_t)k * a.n + i];
+            const uint32_t r = s_rec[w][k][lane];
             put(k, r >> 16, r & 0xFFFFu);
         }
     } else {
