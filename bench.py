@@ -120,7 +120,15 @@ def make_dispatch_workload(n, device, g):
     k = n * DISPATCH_SUBS
     # algorithmic bytes: offset, status and container header byte per datagram;
     # u16 size + header byte read and {start, len, parent} (16 B) written per packet
+    # the walk's HBM floor: every 64-B sector holding a byte it must read (header
+    # byte, each entry's u16 size + header byte), once per container
+    need = np.array([0] + [b for j in range(DISPATCH_SUBS) for b in range(1 + j * DISPATCH_SUB, 4 + j * DISPATCH_SUB)])
+    starts = np.arange(n, dtype=np.int64)[:, None] * S
+    lines = (starts + need[None, :]) // 64
+    per = 1 + (np.diff(lines, axis=1) != 0).sum(axis=1)
+    line_bytes = int(per.sum()) * 64 + n * (8 + 1) + k * 16
     return dict(data=data, n=n, L=None, off=off, payload=n * S, algo=n * (8 + 1 + 1) + k * (3 + 16),
+                line_bytes=line_bytes,
                 dispatch=True, status=status, pkts=k,
                 pkt_start=torch.empty(k, dtype=torch.int64, device=device),
                 pkt_len=torch.empty(k, dtype=torch.int32, device=device),
@@ -303,6 +311,11 @@ def main():
                 "kernel_ms": round(kern_ms, 5),
             },
         }
+        if "line_bytes" in w:  # random narrow reads: HBM moves whole 64-B sectors
+            lb = w["line_bytes"] / (kern_ms * 1e-3) / 1e9
+            line["roofline"]["sector_granular_bytes_per_launch"] = w["line_bytes"]
+            line["roofline"]["sector_granular_achieved"] = round(lb, 1)
+            line["roofline"]["sector_granular_frac"] = round(lb / HBM_PEAK_GBS, 4)
         probe = hbm_probe_peak(w["data"], device)
         if probe:
             line["roofline"]["measured_stream_read_peak_gbs"] = round(probe, 1)

@@ -74,6 +74,7 @@ struct BucketArgs {
     uint32_t* counts;
     uint32_t* fill;   // counts + kCounterCopies * kBuckets
     uint4* desc;      // BatchArgs::desc layout, 16-byte aligned
+    uint32_t spread;  // window layout: M, windows visited in M sweeps (0: in order)
 };
 
 // scratch words (u32) for a bucketed batch of n datagrams, and its layout

@@ -60,6 +60,8 @@ __device__ inline uint32_t load3(const uint8_t* q) {
 template <typename F>
 __device__ inline uint32_t walk(const DispatchArgs& a, uint64_t s, uint32_t size, F&& emit) {
     const uint8_t* p = a.base + s;
+    // the header byte and the first entry of a container share a round trip
+    uint32_t v = size >= 3u ? load3(p + 1) : 0u;
     if ((p[0] & 0x1Fu) != kMergedProperty) {
         emit(0u, size);
         return 1;
@@ -67,7 +69,7 @@ __device__ inline uint32_t walk(const DispatchArgs& a, uint64_t s, uint32_t size
     uint32_t pos = 1, c = 0;
     while (pos < size) {
         if (pos + 2u > size) break;
-        const uint32_t v = load3(p + pos);
+        if (pos != 1u) v = load3(p + pos);
         const uint32_t L = v & 0xFFFFu;
         pos += 2;
         if (L > size - pos) break;
@@ -86,9 +88,11 @@ __global__ __launch_bounds__(256) void dispatch_count_kernel(DispatchArgs a) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= a.n) return;
     uint32_t c = 0;
-    if (a.status[i] == 1u) {  // LNL_INBOUND_ACCEPT only
-        const uint64_t s = a.off[i] - a.off0;
-        const uint32_t size = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;  // CRC stripped
+    const uint8_t st = a.status[i];  // issued together with the offsets
+    const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
+    if (st == 1u) {  // LNL_INBOUND_ACCEPT only
+        const uint64_t s = o0 - a.off0;
+        const uint32_t size = (uint32_t)(o1 - o0) - 4u;  // CRC stripped
         uint32_t k = 0;
         c = walk(a, s, size, [&](uint32_t pos, uint32_t len) {
             if (k < kDispatchRec) a.rec[(size_t)k * a.n + i] = (pos << 16) | len;
