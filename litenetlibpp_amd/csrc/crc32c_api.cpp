@@ -661,6 +661,38 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
     a.n = n;
     a.key_len = (uint32_t)key_len;
     memcpy(a.key, key, key_len);
+    // fixed stride, stride >= 16, 16-byte aligned: the flat kernel (whole pieces
+    // per lane, coalesced); LNL_XOR_FLAT=0 keeps the per-datagram kernel
+    static const int flat_v = [] {
+        const char* e = getenv("LNL_XOR_FLAT");
+        return e ? atoi(e) : 6;  // 2 pieces in flight, nontemporal
+    }();
+    static const int flat_wg = [] {
+        const char* e = getenv("LNL_XOR_FLAT_WG");  // workgroups per CU
+        return e ? std::max(1, atoi(e)) : 8;
+    }();
+    const bool flat_on = flat_v > 0;
+    const uint64_t span = d_off ? 0 : (uint64_t)(n - 1) * stride + len;
+    if (flat_on && !d_off && stride >= 16 && stride < (1u << 31) && len >= 1 &&
+        ((uintptr_t)d_base & 15u) == 0 && span < (1ull << 35)) {
+        lnl::FlatArgs f{};
+        f.span = span;
+        f.pieces = (uint32_t)((span + 15) / 16);
+        f.whole = (uint32_t)(span / 16);
+        f.S = (uint32_t)stride;
+        f.L = len;
+        f.K = (uint32_t)key_len;
+        f.n = n;
+        f.SK = f.S % f.K;
+        const uint32_t per = 256u * 4u;  // pieces per workgroup per step (kThreads x kUnroll)
+        const uint32_t grid = std::max(1u, std::min((f.pieces + per - 1) / per, (uint32_t)S->cus * (uint32_t)flat_wg));
+        const uint64_t step = 16ull * grid * 256u;
+        f.sd = (uint32_t)(step / f.S);
+        f.sr = (uint32_t)(step % f.S);
+        f.srk = f.sr % f.K;
+        hipError_t e = lnl::launch_xor_flat(a, f, (int)grid, flat_v, (hipStream_t)hip_stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "xor flat launch");
+    }
     // lnl::kXorPerWg datagrams per workgroup (uncapped grid: measured faster than persistent)
     const uint32_t wgs = (n + lnl::kXorPerWg - 1u) / lnl::kXorPerWg;
 #ifndef LNL_XOR_WG_PER_CU

@@ -341,11 +341,23 @@ __global__ __launch_bounds__(kWinThreads) void bucket_window_kernel(BucketArgs a
         const uint32_t w = blockIdx.x;
         if (K > 1u && w < K * M) d0 = ((w % M) * K + w / M) * W;
     }
+    // XCD placement (a.xcd): the window's batches go to batch indices that the
+    // persistent grid's first round gives to one XCD (workgroups round-robin
+    // over 8 XCDs, 4 waves each), so the boundary lines two neighbouring
+    // datagrams share meet in one L2.  Slot s = 8 g + x of a full group of 8:
+    // batch q of the window -> 256 g + 32 (q / 4) + 4 x + q % 4.
+    constexpr uint32_t kWB = kWinThreads * kPT / 64u;  // batches per window
+    const uint32_t slot = d0 / (kWinThreads * kPT);
+    const bool xmap = a.xcd && kWB == 32u && slot < (a.n / (kWinThreads * kPT)) / 8u * 8u;
 #pragma unroll
     for (int j = 0; j < kPT; ++j) {
         const uint32_t i = w0 + threadIdx.x + j * kWinThreads;
+        const uint32_t r = basek[key[j]] + rank[j];
+        const uint32_t q = r >> 6;
+        const uint32_t pos = xmap ? 64u * (256u * (slot >> 3) + 32u * (q >> 2) + 4u * (slot & 7u) + (q & 3u)) + (r & 63u)
+                                  : d0 + r;
         if (i < a.n)
-            a.desc[d0 + basek[key[j]] + rank[j]] =
+            a.desc[pos] =
                 make_uint4(i, len[j], (uint32_t)start[j], (uint32_t)(start[j] >> 32));
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl[0] = a.n;
@@ -560,6 +572,7 @@ hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream) {
         const dim3 g((a.n + kWinThreads * pt - 1) / (kWinThreads * pt));
         BucketArgs b = a;
         b.spread = 4u;
+        if (const char* e = getenv("LNL_BUCKET_XCD")) b.xcd = (uint32_t)atoi(e);
         if (const char* e = getenv("LNL_BUCKET_SPREAD")) b.spread = (uint32_t)atoi(e);
         if (pt == 2u) hipLaunchKernelGGL(bucket_window_kernel<2>, g, dim3(kWinThreads), 0, stream, b);
         if (pt == 4u) hipLaunchKernelGGL(bucket_window_kernel<4>, g, dim3(kWinThreads), 0, stream, b);

@@ -75,6 +75,7 @@ struct BucketArgs {
     uint32_t* fill;   // counts + kCounterCopies * kBuckets
     uint4* desc;      // BatchArgs::desc layout, 16-byte aligned
     uint32_t spread;  // window layout: M, windows visited in M sweeps (0: in order)
+    uint32_t xcd;     // window layout: a window's batches on one XCD (W = 2048 only)
 };
 
 // scratch words (u32) for a bucketed batch of n datagrams, and its layout
@@ -202,6 +203,16 @@ struct XorArgs {
     uint8_t key[kXorMaxKey];
 };
 hipError_t launch_xor_layer(const XorArgs& a, int grid, hipStream_t stream);
+// flat fixed-stride XOR (lnl_xor.hip): host-precomputed stepping constants
+struct FlatArgs {
+    uint64_t span;    // (n - 1) * stride + len bytes
+    uint32_t pieces;  // ceil(span / 16)
+    uint32_t whole;   // floor(span / 16): pieces entirely inside the span
+    uint32_t S, L, K, n;
+    uint32_t SK;              // S % K
+    uint32_t sd, sr, srk;     // one grid-stride step of 16 T bytes: / S, % S, (% S) % K
+};
+hipError_t launch_xor_flat(const XorArgs& a, const FlatArgs& f, int grid, int variant, hipStream_t stream);
 
 // Delivered packets of a filtered burst (lnl_dispatch.hip): accepted
 // datagrams, MERGED containers cut into their packets.

@@ -24,6 +24,10 @@
 // Key bytes come from LDS: four copies of the periodic key stream shifted by
 // 0..3 bytes, so the 16 key bytes of any phase m are four aligned dword reads
 // from copy m & 3.
+//
+// Fixed strides >= 16 over a 16-byte aligned base take the flat kernel below
+// instead (whole pieces per lane, no shared edges): 0.502 ms on the config-2
+// batch, 5.86 TB/s read + write, with 2 pieces in flight and nt loads/stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -47,9 +51,10 @@ constexpr int kGroup = LNL_XOR_GROUP;
 constexpr int kUnroll = LNL_XOR_UNROLL;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(kThreads) void xor_layer_kernel(XorArgs a) {
-    // key stream copies: S_s[i] = key[(i + s) % K], i < K + 20 (bytes), s = 0..3
-    __shared__ uint32_t ks[4][(kXorMaxKey + 20 + 3) / 4];
+constexpr uint32_t kKeyWords = (kXorMaxKey + 20 + 3) / 4;
+
+// key stream copies: ks[s][i] bytes = key[(i + s) % K], i < K + 20, s = 0..3
+__device__ inline void stage_key(const XorArgs& a, uint32_t (*ks)[kKeyWords]) {
     const uint32_t K = a.key_len;
     const uint32_t words = (K + 20 + 3) / 4;
     for (uint32_t t = threadIdx.x; t < 4 * words; t += kThreads) {
@@ -58,6 +63,30 @@ __global__ __launch_bounds__(kThreads) void xor_layer_kernel(XorArgs a) {
         for (uint32_t b = 0; b < 4; ++b) v |= (uint32_t)a.key[(4 * w + b + s) % K] << (8 * b);
         ks[s][w] = v;
     }
+}
+
+// the 16 key-stream bytes starting at phase m (< K)
+__device__ inline u32x4 key_at(const uint32_t (*ks)[kKeyWords], uint32_t m) {
+    const uint32_t* kw = &ks[m & 3u][m >> 2];
+    return u32x4{kw[0], kw[1], kw[2], kw[3]};
+}
+
+// bytes [lo, hi) of a 16-byte piece, as four dword masks
+__device__ inline u32x4 byte_range(int lo, int hi) {
+    u32x4 m;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int l = min(max(lo - 4 * w, 0), 4), h = min(max(hi - 4 * w, 0), 4);
+        m[w] = h > l ? (uint32_t)((1ull << (8 * h)) - (1ull << (8 * l))) : 0u;
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(kThreads) void xor_layer_kernel(XorArgs a) {
+    // key stream copies: S_s[i] = key[(i + s) % K], i < K + 20 (bytes), s = 0..3
+    __shared__ uint32_t ks[4][kKeyWords];
+    const uint32_t K = a.key_len;
+    stage_key(a, ks);
     __syncthreads();
 
     const uint32_t groups = gridDim.x * (kThreads / kGroup);
@@ -130,7 +159,113 @@ __global__ __launch_bounds__(kThreads) void xor_layer_kernel(XorArgs a) {
     }
 }
 
+
+// Flat fixed-stride kernel (stride >= 16, len <= stride, 16-byte aligned base):
+// the batch is one byte range, cut into 16-byte pieces that consecutive lanes
+// own whole -- every load and store is a coalesced dwordx4, and no piece is
+// shared, so there are no byte-store edges.  A lane tracks, for its piece at
+// byte 16k, the datagram d, the offset r = 16k - d*stride and the key phase
+// r % K incrementally over its grid-stride steps (no division in the loop).
+// The key of a piece is the key stream at phase r % K up to the datagram's end
+// (or the gap after it), then the stream at phase 0 for the next datagram.
+struct FlatState {
+    uint32_t d, r, ph;
+};
+
+__device__ inline void flat_step(FlatState& st, const FlatArgs& f) {
+    st.d += f.sd;
+    st.r += f.sr;
+    st.ph += f.srk;
+    if (st.ph >= f.K) st.ph -= f.K;
+    if (st.r >= f.S) {
+        st.r -= f.S;
+        st.d += 1u;
+        st.ph = st.ph >= f.SK ? st.ph - f.SK : st.ph + f.K - f.SK;
+    }
+}
+
+__device__ inline u32x4 flat_key(const uint32_t (*ks)[kKeyWords], const FlatArgs& f, const FlatState& st) {
+    const uint32_t L = f.L;
+    if (st.d < f.n && st.r + 16u <= L) return key_at(ks, st.ph);  // whole piece in one datagram
+    // bytes [0, ca) belong to datagram d (offsets r.. < L), bytes [bc, hb) to d + 1
+    int ca = 0, bc = 16, hb = 16;
+    if (st.d < f.n && st.r < L) ca = (int)min(L - st.r, 16u);
+    if (f.S - st.r < 16u && st.d + 1u < f.n) {
+        bc = (int)(f.S - st.r);
+        hb = (int)min((uint32_t)bc + L, 16u);
+    }
+    const u32x4 mA = byte_range(0, ca), mB = byte_range(bc, hb);
+    u32x4 k = key_at(ks, st.ph) & mA;
+    if (hb > bc) {
+        const uint32_t m2 = (f.K - (uint32_t)bc % f.K) % f.K;  // byte b >= bc: key[(b - bc) % K]
+        k |= key_at(ks, m2) & mB;
+    }
+    return k;
+}
+
+template <int kU, bool kNT>
+__global__ __launch_bounds__(kThreads) void xor_flat_kernel(XorArgs a, FlatArgs f) {
+    __shared__ uint32_t ks[4][kKeyWords];
+    stage_key(a, ks);
+    __syncthreads();
+    const uint32_t T = gridDim.x * kThreads;
+    const uint32_t k0 = blockIdx.x * kThreads + threadIdx.x;
+    if (k0 >= f.pieces) return;
+    FlatState st;
+    {
+        const uint64_t o = 16ull * k0;
+        st.d = (uint32_t)(o / f.S);
+        st.r = (uint32_t)(o - (uint64_t)st.d * f.S);
+        st.ph = st.r % f.K;
+    }
+    u32x4* const base = reinterpret_cast<u32x4*>(a.base);
+    for (uint32_t k = k0; k < f.pieces; k += kU * T) {
+        u32x4 v[kU];
+        FlatState sts[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            sts[u] = st;
+            if (k + u * T < f.whole) {
+                if constexpr (kNT)
+                    v[u] = __builtin_nontemporal_load(base + k + u * T);
+                else
+                    v[u] = base[k + u * T];
+            }
+            flat_step(st, f);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t q = k + u * T;
+            if (q >= f.pieces) break;
+            const u32x4 key = flat_key(ks, f, sts[u]);
+            if (q < f.whole) {
+                if constexpr (kNT)
+                    __builtin_nontemporal_store(v[u] ^ key, base + q);
+                else
+                    base[q] = v[u] ^ key;
+            } else {  // the last piece runs past the batch: its own bytes only
+                uint8_t* bp = a.base + 16ull * q;
+                const uint32_t kw[4] = {key.x, key.y, key.z, key.w};
+                for (uint32_t j = 0; j < 16u && 16ull * q + j < f.span; ++j)
+                    bp[j] ^= (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
+            }
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_xor_flat(const XorArgs& a, const FlatArgs& f, int grid, int variant, hipStream_t stream) {
+    switch (variant) {  // pieces in flight per lane x cache policy (measured in DESIGN 5)
+        case 2: hipLaunchKernelGGL((xor_flat_kernel<4, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        case 3: hipLaunchKernelGGL((xor_flat_kernel<8, false>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        case 4: hipLaunchKernelGGL((xor_flat_kernel<8, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        case 5: hipLaunchKernelGGL((xor_flat_kernel<2, false>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        case 6: hipLaunchKernelGGL((xor_flat_kernel<2, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        default: hipLaunchKernelGGL((xor_flat_kernel<4, false>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_xor_layer(const XorArgs& a, int grid, hipStream_t stream) {
     hipLaunchKernelGGL(xor_layer_kernel, dim3(grid), dim3(kThreads), 0, stream, a);

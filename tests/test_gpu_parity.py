@@ -610,17 +610,41 @@ def test_xor_layer_csr(P, klen):
     assert np.array_equal(d.cpu().numpy(), data)
 
 
-@pytest.mark.parametrize("stride,length", [(1400, 1400), (1408, 1400), (64, 17), (1432, 1)])
-def test_xor_layer_fixed(P, stride, length):
-    rng = np.random.default_rng(stride + length)
-    key = b"LiteNetLib"
+@pytest.mark.parametrize("stride,length,klen,shift", [
+    (1400, 1400, 10, 0), (1408, 1400, 10, 0), (64, 17, 10, 0), (1432, 1, 10, 0),
+    (16, 16, 3, 0), (17, 17, 256, 0), (17, 5, 1, 0), (33, 32, 37, 0), (1400, 1400, 22, 0),
+    (15, 15, 4, 0), (1400, 1400, 22, 3), (100, 64, 16, 1)])
+def test_xor_layer_fixed(P, stride, length, klen, shift):
+    """Fixed-stride XOR layer in place: the flat kernel (stride >= 16, 16-byte
+    aligned base; pieces that straddle two datagrams, gaps between them, a last
+    piece past the batch) and the per-datagram kernel (stride < 16, unaligned
+    base: shift > 0) against the restatement; gap bytes stay untouched."""
+    rng = np.random.default_rng(stride + length + klen)
+    key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
     n = 5000
-    data = rng.integers(0, 256, n * stride + 16, dtype=np.uint8)
-    d = dev(data)
+    data = rng.integers(0, 256, n * stride + 16 + shift, dtype=np.uint8)
+    full = dev(data)
+    d = full[shift:]
     P.xor_layer_fixed(d, stride, length, n, key)
     exp = data.copy()
     for i in range(n):
-        exp[i * stride:i * stride + length] = oracle.xor_layer(data[i * stride:i * stride + length], key)
+        a = shift + i * stride
+        exp[a:a + length] = oracle.xor_layer(data[a:a + length], key)
+    assert np.array_equal(full.cpu().numpy(), exp)
+
+
+def test_xor_layer_fixed_full_config2(P):
+    """The bench workload at full size (2^20 x 1400 B, 22-byte key): every byte
+    against a vectorised restatement (key stream per datagram, tiled)."""
+    n, L = 1 << 20, 1400
+    key = b"LiteNetLibPP-bench-key"
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    data = d.cpu().numpy()
+    P.xor_layer_fixed(d, L, L, n, key)
+    ks = np.frombuffer(key, np.uint8)[np.arange(L) % len(key)]
+    exp = (data.reshape(n, L) ^ ks[None, :]).reshape(-1)
     assert np.array_equal(d.cpu().numpy(), exp)
 
 
