@@ -12,7 +12,7 @@ for w in csr filter xor dispatch; do
 done
 timeout -k 10 300 python -u bench.py --workload csr --host-path > gpurun_out/final_csr_host.json 2> gpurun_out/final_csr_host.err || exit 1
 # summaries on the box (the rocprof databases are too big to copy back)
-for w in fixed csr filter dispatch; do
+for w in fixed csr filter dispatch xor; do
   timeout -k 10 900 bash tools/profile_round.sh $TAG $w || exit 1
   PROFILES_DIR=gpurun_out/profiles_$TAG python3 tools/write_profiles.py $TAG $w > /dev/null || exit 1
   rm -rf gpurun_out/prof_${TAG}_$w
