@@ -16,13 +16,20 @@
 //
 //   hipcc -O2 -std=c++17 examples/socket_path.cpp -Llitenetlibpp_amd -llnl_crc32c \
 //         -Wl,-rpath,$PWD/litenetlibpp_amd -o socket_path
-//   ./socket_path [--count N] [--burst B] [--corrupt K] [--device D]
+//   ./socket_path [--count N] [--burst B] [--corrupt K] [--device D] [--receivers R]
+//
+// --receivers R: R receive sockets bound to
+// one port with SO_REUSEPORT, one receiver thread each with its own pinned
+// burst buffer, fed by R sender sockets (the kernel spreads flows over the
+// sockets by 4-tuple hash).  The host filter serialises GPU use per device,
+// so while one thread's burst is on the GPU the others keep receiving.
 #include <arpa/inet.h>
 #include <hip/hip_runtime.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -44,6 +51,7 @@ struct Opts {
     uint32_t burst = 1024;
     uint32_t corrupt = 50;
     int device = 0;
+    uint32_t receivers = 1;
 };
 
 Opts parse(int argc, char** argv) {
@@ -55,6 +63,7 @@ Opts parse(int argc, char** argv) {
         else if (k == "--burst") o.burst = (uint32_t)v;
         else if (k == "--corrupt") o.corrupt = (uint32_t)v;
         else if (k == "--device") o.device = (int)v;
+        else if (k == "--receivers") o.receivers = (uint32_t)std::max(1L, std::min(v, 64L));
     }
     return o;
 }
@@ -84,80 +93,124 @@ int main(int argc, char** argv) {
     const Opts o = parse(argc, argv);
     const auto wire = make_wire(o.count, o.corrupt);
 
-    int rx = socket(AF_INET, SOCK_DGRAM, 0), tx = socket(AF_INET, SOCK_DGRAM, 0);
-    int rcvbuf = 1 << 26;
-    setsockopt(rx, SOL_SOCKET, SO_RCVBUF, &rcvbuf, sizeof rcvbuf);
+    const uint32_t R = o.receivers;
+    std::vector<int> rx(R), tx(R);
     sockaddr_in a{};
     a.sin_family = AF_INET;
     a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-    if (bind(rx, (sockaddr*)&a, sizeof a) != 0) return perror("bind"), 1;
-    socklen_t al = sizeof a;
-    getsockname(rx, (sockaddr*)&a, &al);
-    if (connect(tx, (sockaddr*)&a, sizeof a) != 0) return perror("connect"), 1;
-
-    uint8_t* buf = nullptr;  // pinned burst buffer
-    const size_t cap = (size_t)o.burst * LNL_INGRESS_SLOT;
-    if (hipSetDevice(o.device) != hipSuccess || hipHostMalloc((void**)&buf, cap) != hipSuccess) {
-        fprintf(stderr, "no HIP device for the pinned burst buffer\n");
+    for (uint32_t r = 0; r < R; ++r) {
+        rx[r] = socket(AF_INET, SOCK_DGRAM, 0);
+        int one = 1, rcvbuf = 1 << 26;
+        setsockopt(rx[r], SOL_SOCKET, SO_RCVBUF, &rcvbuf, sizeof rcvbuf);
+        if (R > 1) setsockopt(rx[r], SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+        if (bind(rx[r], (sockaddr*)&a, sizeof a) != 0) return perror("bind"), 1;
+        if (r == 0) {  // the others join the port the first one got
+            socklen_t al = sizeof a;
+            getsockname(rx[0], (sockaddr*)&a, &al);
+        }
+    }
+    for (uint32_t r = 0; r < R; ++r) {
+        tx[r] = socket(AF_INET, SOCK_DGRAM, 0);
+        if (connect(tx[r], (sockaddr*)&a, sizeof a) != 0) return perror("connect"), 1;
+    }
+    if (hipSetDevice(o.device) != hipSuccess) {
+        fprintf(stderr, "no HIP device for the pinned burst buffers\n");
         return 2;
     }
-    std::vector<uint64_t> off(o.burst + 1);
-    std::vector<uint8_t> status(o.burst);
 
-    std::atomic<bool> done{false};
-    std::thread sender([&] {  // sendmmsg bursts of 64, paced by the socket buffer
-        std::vector<mmsghdr> m(64);
-        std::vector<iovec> iov(64);
-        for (uint32_t i = 0; i < o.count;) {
-            const uint32_t k = std::min<uint32_t>(64, o.count - i);
-            for (uint32_t j = 0; j < k; ++j) {
-                iov[j] = {(void*)wire[i + j].data(), wire[i + j].size()};
-                memset(&m[j].msg_hdr, 0, sizeof m[j].msg_hdr);
-                m[j].msg_hdr.msg_iov = &iov[j];
-                m[j].msg_hdr.msg_iovlen = 1;
+    std::atomic<uint32_t> senders_left{R};
+    std::vector<std::thread> senders;
+    for (uint32_t r = 0; r < R; ++r)
+        senders.emplace_back([&, r] {  // sendmmsg bursts of 64 (datagrams r, r + R, ...), paced by the socket buffer
+            std::vector<mmsghdr> m(64);
+            std::vector<iovec> iov(64);
+            std::vector<uint32_t> mine;
+            for (uint32_t i = r; i < o.count; i += R) mine.push_back(i);
+            for (size_t i = 0; i < mine.size();) {
+                const uint32_t k = (uint32_t)std::min<size_t>(64, mine.size() - i);
+                for (uint32_t j = 0; j < k; ++j) {
+                    const auto& w = wire[mine[i + j]];
+                    iov[j] = {(void*)w.data(), w.size()};
+                    memset(&m[j].msg_hdr, 0, sizeof m[j].msg_hdr);
+                    m[j].msg_hdr.msg_iov = &iov[j];
+                    m[j].msg_hdr.msg_iovlen = 1;
+                }
+                const int n = sendmmsg(tx[r], m.data(), k, 0);
+                if (n > 0) i += (size_t)n;
+                else std::this_thread::yield();
             }
-            const int r = sendmmsg(tx, m.data(), k, 0);
-            if (r > 0) i += (uint32_t)r;
-            else std::this_thread::yield();
-        }
-        done = true;
-    });
+            --senders_left;
+        });
 
-    uint64_t got = 0, bytes = 0, counts[3] = {0, 0, 0}, mismatch = 0;
-    double t_ingress = 0, t_filter = 0;
+    std::atomic<uint64_t> got{0}, bytes{0}, c0{0}, c1{0}, c2{0}, mismatch{0};
+    std::atomic<int> fail{0};
+    std::vector<double> t_ingress(R, 0.0), t_filter(R, 0.0);
     const auto t0 = clk::now();
-    while (true) {
-        const auto a0 = clk::now();
-        const int n = lnl_ingress_recv_batch(rx, buf, cap, off.data(), o.burst, nullptr, done ? 50 : 200);
-        const auto a1 = clk::now();
-        if (n < 0) return fprintf(stderr, "ingress: %d\n", n), 1;
-        if (n == 0) {
-            if (done) break;
-            continue;
-        }
-        t_ingress += std::chrono::duration<double>(a1 - a0).count();
-        const int rc = lnl_inbound_filter_host(buf, off.data(), (uint32_t)n, status.data(), o.device);
-        t_filter += std::chrono::duration<double>(clk::now() - a1).count();
-        if (rc) return fprintf(stderr, "filter: %d %s\n", rc, lnl_crc32c_last_error()), 1;
-        for (int i = 0; i < n; ++i) {
-            const uint8_t s = status[i];
-            if (s <= 2) ++counts[s];
-            if (s != (uint8_t)lnl_inbound_status(buf + off[i], off[i + 1] - off[i])) ++mismatch;
-        }
-        got += (uint64_t)n;
-        bytes += off[n];
-    }
+    std::vector<std::thread> receivers;
+    for (uint32_t r = 0; r < R; ++r)
+        receivers.emplace_back([&, r] {
+            uint8_t* buf = nullptr;  // this thread's pinned burst buffer
+            const size_t cap = (size_t)o.burst * LNL_INGRESS_SLOT;
+            if (hipSetDevice(o.device) != hipSuccess || hipHostMalloc((void**)&buf, cap) != hipSuccess) {
+                fail = 2;
+                return;
+            }
+            std::vector<uint64_t> off(o.burst + 1);
+            std::vector<uint8_t> status(o.burst);
+            while (true) {
+                const bool done = senders_left.load() == 0;
+                const auto a0 = clk::now();
+                const int n = lnl_ingress_recv_batch(rx[r], buf, cap, off.data(), o.burst, nullptr, done ? 50 : 200);
+                const auto a1 = clk::now();
+                if (n < 0) {
+                    fprintf(stderr, "ingress: %d\n", n);
+                    fail = 1;
+                    break;
+                }
+                if (n == 0) {
+                    if (done) break;
+                    continue;
+                }
+                t_ingress[r] += std::chrono::duration<double>(a1 - a0).count();
+                const int rc = lnl_inbound_filter_host(buf, off.data(), (uint32_t)n, status.data(), o.device);
+                t_filter[r] += std::chrono::duration<double>(clk::now() - a1).count();
+                if (rc) {
+                    fprintf(stderr, "filter: %d %s\n", rc, lnl_crc32c_last_error());
+                    fail = 1;
+                    break;
+                }
+                uint64_t cnt[3] = {0, 0, 0}, bad = 0;
+                for (int i = 0; i < n; ++i) {
+                    const uint8_t s = status[i];
+                    if (s <= 2) ++cnt[s];
+                    if (s != (uint8_t)lnl_inbound_status(buf + off[i], off[i + 1] - off[i])) ++bad;
+                }
+                c0 += cnt[0];
+                c1 += cnt[1];
+                c2 += cnt[2];
+                mismatch += bad;
+                got += (uint64_t)n;
+                bytes += off[n];
+            }
+            (void)hipHostFree(buf);
+        });
+    for (auto& t : receivers) t.join();
     const double wall = std::chrono::duration<double>(clk::now() - t0).count();
-    sender.join();
-    printf("{\"sent\": %u, \"received\": %llu, \"bytes\": %llu, \"burst\": %u, "
+    for (auto& t : senders) t.join();
+    if (fail) return fail.load();
+    double ti = 0, tf = 0, tboth = 0;  // slowest receiver
+    for (uint32_t r = 0; r < R; ++r)
+        ti = std::max(ti, t_ingress[r]), tf = std::max(tf, t_filter[r]), tboth = std::max(tboth, t_ingress[r] + t_filter[r]);
+    // single receiver: ingress-only and ingress + filter rates from the per-burst
+    // times; several: the aggregate over the wall time of the whole run
+    printf("{\"sent\": %u, \"received\": %llu, \"bytes\": %llu, \"burst\": %u, \"receivers\": %u, "
            "\"ingress_s\": %.4f, \"filter_s\": %.4f, \"wall_s\": %.4f, "
-           "\"ingress_gbps\": %.3f, \"ingress_plus_gpu_filter_gbps\": %.3f, "
+           "\"ingress_gbps\": %.3f, \"ingress_plus_gpu_filter_gbps\": %.3f, \"aggregate_wall_gbps\": %.3f, "
            "\"accept\": %llu, \"drop_crc\": %llu, \"malformed\": %llu, \"gpu_cpu_mismatch\": %llu}\n",
-           o.count, (unsigned long long)got, (unsigned long long)bytes, o.burst, t_ingress, t_filter, wall,
-           bytes / t_ingress / 1e9, bytes / (t_ingress + t_filter) / 1e9, (unsigned long long)counts[1],
-           (unsigned long long)counts[0], (unsigned long long)counts[2], (unsigned long long)mismatch);
-    (void)hipHostFree(buf);
-    close(rx);
-    close(tx);
-    return mismatch ? 3 : 0;
+           o.count, (unsigned long long)got.load(), (unsigned long long)bytes.load(), o.burst, R, ti, tf, wall,
+           bytes.load() / ti / 1e9, bytes.load() / tboth / 1e9, bytes.load() / wall / 1e9,
+           (unsigned long long)c1.load(), (unsigned long long)c0.load(), (unsigned long long)c2.load(),
+           (unsigned long long)mismatch.load());
+    for (uint32_t r = 0; r < R; ++r) close(rx[r]), close(tx[r]);
+    return mismatch.load() ? 3 : 0;
 }

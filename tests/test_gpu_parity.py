@@ -20,6 +20,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -459,6 +460,24 @@ def test_host_multi_device_path(P, devices):
     pinned = torch.from_numpy(data).pin_memory().numpy()
     got = P.batch_host_multi(pinned, off, devices)
     assert np.array_equal(got, oracle.batch_csr(data, off))
+
+
+@pytest.mark.parametrize("receivers", [1, 3])
+def test_socket_example_receivers(P, receivers):
+    """examples/socket_path (built by build()): R SO_REUSEPORT receive sockets,
+    one thread and pinned burst buffer each, GPU filter per burst; every GPU
+    status equals lnl_inbound_status on the CPU (exit code 3 otherwise)."""
+    import json
+    import subprocess
+    exe = os.path.join(ROOT, "examples", "socket_path")
+    if not os.path.exists(exe):
+        pytest.fail("examples/socket_path not built (run __graft_entry__.build())")
+    r = subprocess.run([exe, "--count", "30000", "--burst", "1024", "--receivers", str(receivers)],
+                       capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0, r.stderr
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["gpu_cpu_mismatch"] == 0 and j["receivers"] == receivers
+    assert j["received"] >= 0.5 * j["sent"] and j["accept"] > 0 and j["drop_crc"] > 0
 
 
 def test_socket_path_end_to_end(P):
