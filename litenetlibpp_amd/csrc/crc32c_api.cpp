@@ -617,6 +617,36 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     if (cap && (!d_pkt_start || !d_pkt_len || !d_pkt_parent)) return fail(-EINVAL, "NULL output");
     DeviceState* S;
     if (int rc = current_device(&S)) return rc;
+    // LNL_DISPATCH_ONEPASS=1: one launch with a decoupled look-back (experiment,
+    // parity-clean but 0.61 ms against 0.18 for count + scan + emit)
+    static const bool onepass = [] {
+        const char* e = getenv("LNL_DISPATCH_ONEPASS");
+        return e && e[0] == '1';
+    }();
+    if (onepass) {
+        const size_t nwg = ((size_t)n + 255) / 256;
+        void* flags = nullptr;
+        hipError_t e = hipMallocAsync(&flags, nwg * 8, st);
+        if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", nwg * 8, hipGetErrorString(e));
+        lnl::DispatchArgs a{};
+        a.base = d_base;
+        a.off = d_off;
+        a.n = n;
+        a.status = d_status;
+        a.look = (uint64_t*)flags;
+        a.pkt_start = d_pkt_start;
+        a.pkt_len = d_pkt_len;
+        a.pkt_parent = d_pkt_parent;
+        a.cap = cap;
+        a.total = d_total;
+        int rc = 0;
+        e = hipMemsetAsync(flags, 0, nwg * 8, st);
+        if (e != hipSuccess) rc = hip_fail(e, "hipMemsetAsync");
+        if (rc == 0 && (e = lnl::launch_dispatch(a, nullptr, 0, st)) != hipSuccess) rc = hip_fail(e, "dispatch launch");
+        e = hipFreeAsync(flags, st);
+        if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+        return rc;
+    }
     const size_t scan_bytes = lnl::dispatch_scan_bytes(n);
     void* scratch = nullptr;
     const size_t bytes = (2 + (size_t)lnl::kDispatchRec) * n * 4 + scan_bytes + 256;

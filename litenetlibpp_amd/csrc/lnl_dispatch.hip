@@ -173,6 +173,148 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
     }
 }
 
+// One pass (experiment, LNL_DISPATCH_ONEPASS=1): walk, count and write in one launch.  The workgroup's
+// packet offset comes from a decoupled look-back over per-workgroup flags
+// (a.look[b] = flag << 32 | value; flag 1: this workgroup's own count,
+// 2: inclusive prefix), so there is no device-wide scan launch and the
+// records never leave the chip.  Wave 0 reads 64 predecessors' flags per
+// round trip and stops at the nearest inclusive prefix.  Workgroups are
+// dispatched in order, so a predecessor a workgroup waits on is resident or
+// done; the spin is bounded anyway, and a timeout reports total = 0xFFFFFFFF
+// instead of hanging.
+constexpr uint32_t kLookSpin = 1u << 22;
+
+__device__ inline uint64_t look_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void look_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void dispatch_onepass_kernel(DispatchArgs a) {
+    __shared__ uint32_t s_first[4][65];
+    __shared__ uint32_t s_fast[4][64];
+    __shared__ uint64_t s_start[4][64];
+    __shared__ uint32_t s_rec[4][kDispatchRec][64];
+    __shared__ uint32_t s_wsum[4];
+    __shared__ uint32_t s_prefix, s_bad;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t i0 = blockIdx.x * 256u + w * 64u;
+    const uint32_t i = i0 + lane;
+    uint32_t c = 0, size = 0;
+    uint64_t s = 0;
+    if (i < a.n) {
+        const uint8_t st = a.status[i];
+        const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
+        s = o0 - a.off0;
+        if (st == 1u) {  // LNL_INBOUND_ACCEPT only
+            size = (uint32_t)(o1 - o0) - 4u;  // CRC stripped
+            uint32_t k = 0;
+            c = walk(a, s, size, [&](uint32_t pos, uint32_t len) {
+                if (k < kDispatchRec) s_rec[w][k][lane] = (pos << 16) | len;
+                ++k;
+            });
+        }
+    }
+    const bool fast = c <= kDispatchRec && size < 65536u;
+    // workgroup scan of the counts: waves by shuffles, then the 4 wave sums
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+        if (lane >= (uint32_t)d) incl += o;
+    }
+    if (lane == 63u) s_wsum[w] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < 4u; ++v) {
+        wbase += v < w ? s_wsum[v] : 0u;
+        total += s_wsum[v];
+    }
+    if (w == 0u) {  // wave 0 looks back 64 predecessors per round trip
+        const uint32_t b = blockIdx.x;
+        uint32_t prefix = 0, bad = 0;
+        if (b == 0) {
+            if (lane == 0u) look_store(&a.look[0], (2ull << 32) | total);
+        } else {
+            if (lane == 0u) look_store(&a.look[b], (1ull << 32) | total);
+            int64_t j = (int64_t)b - 1;
+            uint32_t spin = 0;
+            while (true) {
+                const int64_t idx = j - (int64_t)lane;
+                const uint64_t v = idx >= 0 ? look_load(&a.look[idx]) : (2ull << 32);  // before 0: prefix 0
+                const uint32_t flag = (uint32_t)(v >> 32);
+                const uint64_t m2 = __ballot(flag == 2u), m0 = __ballot(flag == 0u);
+                const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
+                const uint64_t need = first2 >= 63u ? ~0ull : ((2ull << first2) - 1ull);
+                if (m0 & need) {  // a predecessor this window needs has not published yet
+                    if (++spin > kLookSpin) {
+                        bad = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint32_t part = lane <= first2 ? (uint32_t)v : 0u;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) part += (uint32_t)__shfl_xor((int)part, d, 64);
+                prefix += part;
+                if (first2 < 64u) break;
+                j -= 64;
+            }
+            if (lane == 0u && !bad) look_store(&a.look[b], (2ull << 32) | (prefix + total));
+        }
+        if (lane == 0u) {
+            s_prefix = prefix;
+            s_bad = bad;
+        }
+    }
+    __syncthreads();
+    const uint32_t f = s_prefix + wbase + incl - c;  // first output slot of datagram i
+    if (i + 1u == a.n) *a.total = s_bad ? 0xFFFFFFFFu : f + c;
+    if (s_bad) return;
+    // cooperative, coalesced write of the wave's packets (as dispatch_emit_kernel)
+    s_first[w][lane] = f;  // lanes past n: c = 0, f = the running total
+    if (lane == 63u) s_first[w][64] = f + c;
+    s_fast[w][lane] = fast;
+    s_start[w][lane] = s;
+    __syncthreads();
+    if (i0 >= a.n) return;
+    const uint32_t F0 = s_first[w][0], F1 = s_first[w][64];
+    const bool coop = F1 - F0 <= kEmitMaxSteps * 64u;
+    if (coop) {
+        const uint32_t end = F1 < a.cap ? F1 : a.cap;
+        for (uint32_t j = F0 + lane; j < end; j += 64u) {
+            uint32_t lo = 0;
+            for (uint32_t step = 32; step; step >>= 1)
+                if (s_first[w][lo + step] <= j && lo + step < 64u) lo += step;
+            if (!s_fast[w][lo]) continue;
+            const uint32_t r = s_rec[w][j - s_first[w][lo]][lo];
+            a.pkt_start[j] = s_start[w][lo] + (r >> 16);
+            a.pkt_len[j] = r & 0xFFFFu;
+            a.pkt_parent[j] = i0 + lo;
+        }
+    }
+    if (c == 0u || f >= a.cap || (coop && fast)) return;
+    auto put = [&](uint32_t k, uint32_t pos, uint32_t len) {
+        if (f + k < a.cap) {
+            a.pkt_start[f + k] = s + pos;
+            a.pkt_len[f + k] = len;
+            a.pkt_parent[f + k] = i;
+        }
+    };
+    if (fast) {
+        for (uint32_t k = 0; k < c; ++k) {
+            const uint32_t r = s_rec[w][k][lane];
+            put(k, r >> 16, r & 0xFFFFu);
+        }
+    } else {
+        uint32_t k = 0;
+        walk(a, s, size, [&](uint32_t pos, uint32_t len) { put(k++, pos, len); });
+    }
+}
+
 }  // namespace
 
 size_t dispatch_scan_bytes(uint32_t n) {
@@ -185,6 +327,10 @@ size_t dispatch_scan_bytes(uint32_t n) {
 
 hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream) {
     const dim3 grid((a.n + 255u) / 256u);
+    if (a.look) {  // one pass (flags zeroed by the caller)
+        hipLaunchKernelGGL(dispatch_onepass_kernel, grid, dim3(256), 0, stream, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(dispatch_count_kernel, grid, dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
