@@ -293,8 +293,7 @@ __global__ __launch_bounds__(kThreads) void bucket_place_kernel(BucketArgs a) {
 // histogram or scan, and neighbouring datagrams -- which share a boundary line
 // -- are processed at about the same time.  Descriptor order within a line
 // count follows LDS atomics (the CRCs do not depend on it).
-constexpr int kWinThreads = 512;
-template <int kPT>
+template <int kPT, int kWinThreads = 512>
 __global__ __launch_bounds__(kWinThreads) void bucket_window_kernel(BucketArgs a) {
     __shared__ uint32_t cnt[kBuckets], basek[kBuckets];
     if (threadIdx.x < kBuckets) cnt[threadIdx.x] = 0;
@@ -528,13 +527,13 @@ hipError_t launch_pair_prep(const PairPrepArgs& a, hipStream_t stream) {
 
 
 
-// LNL_BUCKET_WINDOW=1|2|3|4: per-window sort (windows of 2048, 4096, 8192,
-// 1024 datagrams) instead of the global bucket layout
+// LNL_BUCKET_WINDOW=1..6: per-window sort (launch_csr_buckets lists the window
+// sizes and workgroup shapes); 0: the global bucket layout
 int bucket_window() {
     static const int w = [] {
         const char* e = getenv("LNL_BUCKET_WINDOW");
         if (!e) return 1;  // default: windows of 2048
-        return e[0] >= '1' && e[0] <= '4' ? e[0] - '0' : 0;
+        return e[0] >= '1' && e[0] <= '6' ? e[0] - '0' : 0;
     }();
     return w;
 }
@@ -568,16 +567,25 @@ void bucket_layout(BucketArgs& a, uint32_t* w) {
 hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream) {
     const uint32_t groups = (a.n + kBucketPerBlock - 1) / kBucketPerBlock;
     if (LNL_BUCKET_LAYOUT && bucket_window()) {
-        const uint32_t pt = bucket_window() == 4 ? 2u : 4u << (bucket_window() - 1);
-        const dim3 g((a.n + kWinThreads * pt - 1) / (kWinThreads * pt));
+        // 1: W = 2048 with 256 threads (default; 0.174-0.176 ms per config-3 call
+        // against 0.177-0.179 with 512 and 0.175-0.177 with 1024 threads);
+        // 2, 3, 4: W = 4096, 8192, 1024 with 512 threads; 5, 6: W = 2048 with
+        // 1024 / 512 threads
+        const int wv = bucket_window();
+        const uint32_t W = wv == 2 ? 4096u : wv == 3 ? 8192u : wv == 4 ? 1024u : 2048u;
+        const dim3 g((a.n + W - 1) / W);
         BucketArgs b = a;
         b.spread = 4u;
-        if (const char* e = getenv("LNL_BUCKET_XCD")) b.xcd = (uint32_t)atoi(e);
         if (const char* e = getenv("LNL_BUCKET_SPREAD")) b.spread = (uint32_t)atoi(e);
-        if (pt == 2u) hipLaunchKernelGGL(bucket_window_kernel<2>, g, dim3(kWinThreads), 0, stream, b);
-        if (pt == 4u) hipLaunchKernelGGL(bucket_window_kernel<4>, g, dim3(kWinThreads), 0, stream, b);
-        if (pt == 8u) hipLaunchKernelGGL(bucket_window_kernel<8>, g, dim3(kWinThreads), 0, stream, b);
-        if (pt == 16u) hipLaunchKernelGGL(bucket_window_kernel<16>, g, dim3(kWinThreads), 0, stream, b);
+        if (const char* e = getenv("LNL_BUCKET_XCD")) b.xcd = (uint32_t)atoi(e);
+        switch (wv) {
+            case 2: hipLaunchKernelGGL((bucket_window_kernel<8>), g, dim3(512), 0, stream, b); break;
+            case 3: hipLaunchKernelGGL((bucket_window_kernel<16>), g, dim3(512), 0, stream, b); break;
+            case 4: hipLaunchKernelGGL((bucket_window_kernel<2>), g, dim3(512), 0, stream, b); break;
+            case 5: hipLaunchKernelGGL((bucket_window_kernel<2, 1024>), g, dim3(1024), 0, stream, b); break;
+            case 6: hipLaunchKernelGGL((bucket_window_kernel<4>), g, dim3(512), 0, stream, b); break;
+            default: hipLaunchKernelGGL((bucket_window_kernel<8, 256>), g, dim3(256), 0, stream, b); break;
+        }
         return hipGetLastError();
     }
     if (LNL_BUCKET_LAYOUT) {
