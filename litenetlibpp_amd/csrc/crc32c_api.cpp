@@ -623,6 +623,10 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
         const char* e = getenv("LNL_DISPATCH_ONEPASS");
         return e && e[0] == '1';
     }();
+    static const uint32_t nt_stores = [] {
+        const char* e = getenv("LNL_DISPATCH_NT");
+        return e && e[0] == '1' ? 1u : 0u;
+    }();
     if (onepass) {
         const size_t nwg = ((size_t)n + 255) / 256;
         void* flags = nullptr;
@@ -634,6 +638,7 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
         a.n = n;
         a.status = d_status;
         a.look = (uint64_t*)flags;
+        a.nt = nt_stores;
         a.pkt_start = d_pkt_start;
         a.pkt_len = d_pkt_len;
         a.pkt_parent = d_pkt_parent;
@@ -660,6 +665,7 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     a.counts = (uint32_t*)scratch;
     a.first = a.counts + n;
     a.rec = a.first + n;
+    a.nt = nt_stores;
     a.pkt_start = d_pkt_start;
     a.pkt_len = d_pkt_len;
     a.pkt_parent = d_pkt_parent;

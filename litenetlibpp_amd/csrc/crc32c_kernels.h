@@ -226,6 +226,7 @@ struct DispatchArgs {
     uint32_t* first;        // n (scratch): exclusive scan of counts
     uint32_t* rec;          // kDispatchRec * n (scratch): (pos << 16 | len), slot-major
     uint64_t* look;         // one-pass: per-workgroup look-back flags, zeroed (null: two passes)
+    uint32_t nt;            // nontemporal stores for the cooperative packet writes
     uint64_t* pkt_start;    // cap: packet start relative to base
     uint32_t* pkt_len;      // cap
     uint32_t* pkt_parent;   // cap: datagram index

@@ -149,9 +149,15 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
                 if (s_first[w][lo + step] <= j && lo + step < 64u) lo += step;
             if (!s_fast[w][lo]) continue;
             const uint32_t r = s_rec[w][j - s_first[w][lo]][lo];
-            a.pkt_start[j] = s_start[w][lo] + (r >> 16);
-            a.pkt_len[j] = r & 0xFFFFu;
-            a.pkt_parent[j] = i0 + lo;
+            if (a.nt) {
+                __builtin_nontemporal_store(s_start[w][lo] + (r >> 16), a.pkt_start + j);
+                __builtin_nontemporal_store(r & 0xFFFFu, a.pkt_len + j);
+                __builtin_nontemporal_store(i0 + lo, a.pkt_parent + j);
+            } else {
+                a.pkt_start[j] = s_start[w][lo] + (r >> 16);
+                a.pkt_len[j] = r & 0xFFFFu;
+                a.pkt_parent[j] = i0 + lo;
+            }
         }
     }
     if (c == 0u || f >= a.cap || (coop && fast)) return;
@@ -291,9 +297,15 @@ __global__ __launch_bounds__(256) void dispatch_onepass_kernel(DispatchArgs a) {
                 if (s_first[w][lo + step] <= j && lo + step < 64u) lo += step;
             if (!s_fast[w][lo]) continue;
             const uint32_t r = s_rec[w][j - s_first[w][lo]][lo];
-            a.pkt_start[j] = s_start[w][lo] + (r >> 16);
-            a.pkt_len[j] = r & 0xFFFFu;
-            a.pkt_parent[j] = i0 + lo;
+            if (a.nt) {
+                __builtin_nontemporal_store(s_start[w][lo] + (r >> 16), a.pkt_start + j);
+                __builtin_nontemporal_store(r & 0xFFFFu, a.pkt_len + j);
+                __builtin_nontemporal_store(i0 + lo, a.pkt_parent + j);
+            } else {
+                a.pkt_start[j] = s_start[w][lo] + (r >> 16);
+                a.pkt_len[j] = r & 0xFFFFu;
+                a.pkt_parent[j] = i0 + lo;
+            }
         }
     }
     if (c == 0u || f >= a.cap || (coop && fast)) return;
