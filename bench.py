@@ -2,25 +2,37 @@
 """bench.py -- BASELINE.json's metric: CRC32C GB/s (device-resident) over
 2^20 x 1400 B datagrams, bit-exact.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fixed|csr]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fixed|csr|...]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+With --gpus N > 1 and no launcher (WORLD_SIZE unset), this process starts N
+child processes itself -- one per GPU, RANK / LOCAL_RANK / WORLD_SIZE set --
+before anything touches the GPU, and exits with the worst child's status.
+Under a launcher, WORLD_SIZE must equal --gpus.
 
 A step is one launch of the batched CRC-32C kernel over the rank's resident
 shard (config 2: 2^20 x 1400 B per GPU at stride 1400; config 4 = the same per
 GPU at N = 8: weak scaling, packets sharded by contiguous ranges, no
-collective on the data path -- the only collectives are the timing barrier and
-a MAX over per-rank times).  Inputs are generated on the device before the
-timed region.  Rank 0 prints ONE JSON line.
+collective on the data path -- the only collectives are the timing barrier,
+MIN/MAX/SUM over per-rank times and bytes, and a gather of per-rank figures).
+Inputs are generated on the device before the timed region.  `value` = the
+bytes all ranks checksummed / (last rank's finish - first rank's start), on
+the host wall clock, bracketed by a barrier + synchronize on both sides.
+Rank 0 prints ONE JSON line.
 
 roofline: algorithmic bytes per launch = sum(L) + 4 N (datagram bytes read +
 CRC words written; CSR adds 8 N offset bytes; the xor workload reads and writes
-2 sum(L)) over the average launch duration
-measured with one HIP event pair around the K launches on the launch stream;
-peak 8.0 TB/s (MI355X HBM3E nameplate).  traffic: HBM bytes per launch from the rocprofv3 PMC pass
-(profiles/traffic_<workload>.json, FETCH_SIZE x2 gfx950 correction +
-WRITE_SIZE) when present, else null.
+2 sum(L)) over the average launch duration measured with one HIP event pair
+around the K launches on the launch stream; peak 8.0 TB/s (MI355X HBM3E
+nameplate).  traffic: HBM bytes per launch from the builder's rocprofv3 PMC
+passes (profiles/traffic_<workload>.json; FETCH_SIZE x2 gfx950 correction +
+WRITE_SIZE), labelled as such -- it is not measured inside this run.
 cpu_baseline: the oracle's batch CRC (SSE4.2 crc32 instruction, OpenMP) timed
-on this host's cores over a bounded sample of the same batch (rank 0, N = 1).
+on this host over the WHOLE batch (copied to host memory, untimed), on one
+core and on every core this process may run on (rank 0, N = 1); the checker
+also compares the GPU's output for the whole batch with it.
+host_path: config 5 -- the same batch from pinned host memory through
+lnl_crc32c_batch_host (H2D + kernel + D2H on 2 streams), PCIe-inclusive.
 """
 from __future__ import annotations
 
@@ -28,6 +40,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,10 +52,11 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from litenetlibpp_amd.shard import max_over_ranks, shard_range, sum_over_ranks  # noqa: E402
+from litenetlibpp_amd.shard import gather_over_ranks, max_over_ranks, shard_range, sum_over_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E nameplate, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "CRC32C GB/s (device-resident) over 1M×1400B packets; bit-exact"
+DRY = os.environ.get("LNL_BENCH_DRYRUN") == "1"  # CPU plumbing test: no kernels, no device
 
 
 def parse():
@@ -50,25 +65,52 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "dispatch"], default="fixed",
-                    help="fixed: config 2 (the headline); csr: config 3; filter: the batched inbound "
-                         "filter (CRC check + net_packet::verify) over the config-3 batch as wire "
-                         "datagrams; xor: the XOR-encryption layer in place over the config-2 batch; "
+                    help="fixed: config 2 (the headline; config 4 at N = 8); csr: config 3; filter: the "
+                         "batched inbound filter (CRC check + net_packet::verify) over the config-3 batch as "
+                         "wire datagrams; xor: the XOR-encryption layer in place over the config-2 batch; "
                          "dispatch: lnl_dispatch_csr_dev over accepted MERGED containers of 256-B "
                          "messages (the config-1 traffic shape)")
     ap.add_argument("--packets", type=int, default=1 << 20, help="per GPU")
     ap.add_argument("--length", type=int, default=1400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--host-path", action="store_true",
-                    help="also time lnl_crc32c_batch_host (PCIe-inclusive, config 5)")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the config-5 (PCIe-inclusive) measurement")
     return ap.parse_args()
 
 
+# ------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """One child process per GPU, started before this process makes any GPU
+    call (children are fresh interpreters, never an exec of this one)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
+
+
+# ------------------------------------------------------------------ workloads
 def make_workload(args, rank, world, device):
     """Device-resident synthetic shard (generated on the GPU, untimed): rank r
     owns datagrams shard_range(N * world, r, world) of the job's batch."""
+    _, n = shard_range(args.packets * world, rank, world)
+    if DRY:  # plumbing only: nothing is launched
+        return dict(data=None, n=n, L=args.length, off=None, payload=n * args.length,
+                    algo=n * (args.length + 4))
     g = torch.Generator(device=device)
     g.manual_seed(42 + rank)
-    _, n = shard_range(args.packets * world, rank, world)
     if args.workload == "xor":  # read + write every byte in place
         L = args.length
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
@@ -137,6 +179,8 @@ def make_dispatch_workload(n, device, g):
 
 
 def launch(P, w, out, stream):
+    if DRY:
+        return
     if w.get("dispatch"):
         P._lib.check(P.lib().lnl_dispatch_csr_dev(
             w["data"].data_ptr(), w["off"].data_ptr(), w["n"], w["status"].data_ptr(),
@@ -152,77 +196,136 @@ def launch(P, w, out, stream):
         P.batch_csr(w["data"], w["off"], out=out, stream=stream)
 
 
+# ------------------------------------------------------------------ context figures
 def hbm_probe_peak(data, device):
     """Measured read-only streaming rate over the same buffer (context for the
-    nameplate peak)."""
+    nameplate peak): the best of the probe's forms (litenetlibpp_amd/csrc/hbm_probe.hip)."""
     so = os.path.join(ROOT, "litenetlibpp_amd", "libhbm_probe.so")
     if not os.path.exists(so):
         return None
     L = ctypes.CDLL(so)
-    L.lnl_probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    L.lnl_probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int]
+    L.lnl_probe_stream_read.restype = ctypes.c_int
     sink = torch.zeros(4, dtype=torch.int32, device=device)
     s = torch.cuda.current_stream()
-    nbytes = data.numel() // 16 * 16
-    for _ in range(3):
-        L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 10
-    e0.record()
-    for _ in range(reps):
-        L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream)
-    e1.record()
-    torch.cuda.synchronize()
-    return nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    nbytes = data.numel() // 1024 * 1024
+    best = {}
+    for form in (0, 1):
+        for _ in range(3):
+            L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream, form)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        e0.record()
+        for _ in range(reps):
+            L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream, form)
+        e1.record()
+        torch.cuda.synchronize()
+        best[form] = nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    return best
 
 
-def cpu_baseline(w, gpu_out):
-    """Oracle batch CRC on this host over a bounded sample of the same batch;
-    also checks the GPU output on that sample (bit-exact)."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_copy(w):
+    """The rank's batch in host memory (untimed): (bytes, offsets or None)."""
+    data = w["data"].cpu().numpy()
+    off = None if w["off"] is None else w["off"].cpu().numpy().astype(np.uint64)
+    return data, off
+
+
+def cpu_baseline(w, host):
+    """Checker + CPU baseline: the oracle's batch CRC over the WHOLE batch on
+    1 core and on every core this process may run on; median of repeats over
+    ~2 s per thread count.  Returns (figures, oracle output)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle
-    n_s = min(w["n"], 1 << 17)
-    if w["off"] is None:
-        L = w["L"]
-        sample = w["data"][: n_s * L].cpu().numpy()
+    data, off = host
+    if off is None:
+        L, n = w["L"], w["n"]
         def run(th):
-            return oracle.batch_fixed(sample, L, L, n_s, threads=th)
-        sbytes = n_s * L
-        desc = f"{n_s} x {L} B datagrams (first {sbytes / 1e6:.1f} MB of the GPU batch)"
+            return oracle.batch_fixed(data, L, L, n, threads=th)
     else:
-        off = w["off"][: n_s + 1].cpu().numpy().astype(np.uint64)
-        sample = w["data"][: int(off[-1])].cpu().numpy()
         def run(th):
-            return oracle.batch_csr(sample, off, threads=th)
-        sbytes = int(off[-1] - off[0])
-        desc = f"first {n_s} mixed-length datagrams ({sbytes / 1e6:.1f} MB) of the GPU batch"
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
-    res = {}
-    for th in (1, threads):
-        best, ref = None, None
-        t_end = time.perf_counter() + 5.0
+            return oracle.batch_csr(data, off, threads=th)
+    cores = len(os.sched_getaffinity(0))
+    res, ref = {}, None
+    for th in (1, cores):
+        times = []
+        t_end = time.perf_counter() + 2.0
         while True:
             t0 = time.perf_counter()
             ref = run(th)
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-            if time.perf_counter() > t_end:
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() > t_end and len(times) >= 3:
                 break
-        res[th] = (sbytes / best / 1e9, ref)
-    exact = bool(np.array_equal(gpu_out[:n_s], res[threads][1]))
-    return res, threads, desc, exact
+        res[th] = w["payload"] / float(np.median(times)) / 1e9
+    return res, cores, ref
 
 
+def parity_sample(w, out, host):
+    """Checker: the rank's GPU output vs the oracle on its first datagrams."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle
+    data, off = host
+    k = min(w["n"], 1 << 14)
+    got = out[:k].cpu().numpy().view(np.uint32)
+    if off is None:
+        exp = oracle.batch_fixed(data, w["L"], w["L"], k)
+    else:
+        exp = oracle.batch_csr(data, off[: k + 1])
+    return bool(np.array_equal(got, exp)), k
+
+
+def host_path_rate(P, host, w, device):
+    """Config 5: host-resident pinned batch -> lnl_crc32c_batch_host (H2D +
+    kernel + D2H over 2 streams).  PCIe-inclusive; never the headline value."""
+    data, off = host
+    if off is None:
+        off = np.arange(0, (w["n"] + 1) * w["L"], w["L"], dtype=np.uint64)
+    pinned = torch.from_numpy(data).pin_memory().numpy()
+    P.batch_host(pinned, off, device)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        got = P.batch_host(pinned, off, device)
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(w["payload"] / dt / 1e9, 2), "unit": "GB/s",
+            "what": "config 5: the same batch in pinned host memory through lnl_crc32c_batch_host "
+                    "(H2D + kernel + D2H, 2 streams, chunks of <= 64 Ki datagrams / 64 MiB), blocking, "
+                    f"mean of {reps} calls"}, got
+
+
+# ------------------------------------------------------------------ main
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(env_world or "1")
+    if env_world is not None and world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch one rank per GPU "
+                 f"(torchrun --nproc-per-node {args.gpus}) or drop the launcher and let --gpus spawn them")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # Rehearsal knobs (the driver never sets them): LNL_BENCH_BACKEND=gloo and
     # LNL_BENCH_ONE_GPU=1 run N ranks on one GPU to exercise the N > 1 path.
-    backend = os.environ.get("LNL_BENCH_BACKEND", "nccl")
+    backend = "gloo" if DRY else os.environ.get("LNL_BENCH_BACKEND", "nccl")
     gpu = 0 if os.environ.get("LNL_BENCH_ONE_GPU") == "1" else local
-    torch.cuda.set_device(gpu)
-    device = torch.device("cuda", gpu)
+    if DRY:
+        device = torch.device("cpu")
+    else:
+        torch.cuda.set_device(gpu)
+        device = torch.device("cuda", gpu)
     red_dev = device if backend == "nccl" else None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -231,48 +334,81 @@ def main():
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
     import litenetlibpp_amd as P
-    P.lib()
+    if not DRY:
+        P.lib()
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[gpu]) if backend == "nccl" else dist.barrier()
+
+    def sync():
+        if not DRY:
+            torch.cuda.synchronize()
 
     w = make_workload(args, rank, world, device)
-    out = torch.empty(w["n"], dtype=torch.int32, device=device)
+    out = None if DRY else torch.empty(w["n"], dtype=torch.int32, device=device)
     if w.get("filter") and "status" not in w:
         w["status"] = torch.empty(w["n"], dtype=torch.uint8, device=device)
-    stream = torch.cuda.current_stream()
+    stream = None if DRY else torch.cuda.current_stream()
     for _ in range(args.warmup):
         launch(P, w, out, stream)
-    torch.cuda.synchronize()
+    sync()
 
     # K back-to-back launches bracketed by barrier + synchronize; one HIP event
     # pair on the launch stream gives the average launch duration (per-launch
     # event pairs would insert ~11 us of idle between launches)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier(device_ids=[gpu]) if backend == "nccl" else dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record(stream)
+    if not DRY:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    sync()
+    t0 = time.time()
+    if not DRY:
+        e0.record(stream)
     for _ in range(args.steps):
         launch(P, w, out, stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier(device_ids=[gpu]) if backend == "nccl" else dist.barrier()
-    wall = t1 - t0
-    kern_ms = e0.elapsed_time(e1) / args.steps
-    wall = max_over_ranks(wall, red_dev)          # the job takes as long as its slowest rank
-    kern_ms = max_over_ranks(kern_ms, red_dev)
-    ms_per_step = wall / args.steps * 1e3
+    if not DRY:
+        e1.record(stream)
+    sync()
+    t1 = time.time()
+    barrier()
+    kern_ms = e0.elapsed_time(e1) / args.steps if not DRY else (t1 - t0) * 1e3 / max(args.steps, 1)
+    start = -max_over_ranks(-t0, red_dev)   # the first rank's start
+    end = max_over_ranks(t1, red_dev)       # the last rank's finish
+    ms_per_step = (end - start) / args.steps * 1e3
     total_payload = sum_over_ranks(w["payload"], red_dev)
-    value = total_payload / (ms_per_step * 1e-3) / 1e9
-    achieved = w["algo"] / (kern_ms * 1e-3) / 1e9
+    value = total_payload / ((end - start) or 1e-9) / 1e9
+    kern_all = gather_over_ranks(kern_ms, red_dev)
+    kern_max = max(kern_all)
+    achieved = w["algo"] / (kern_max * 1e-3) / 1e9
+
+    # checker, outside the timed region: every rank compares its first
+    # datagrams with the oracle (rank 0 at N = 1: the whole batch, below)
+    crc_workload = not DRY and not (w.get("xor") or w.get("filter") or w.get("dispatch"))
+    host = host_copy(w) if crc_workload else None
+    ok_sample = 1.0
+    if crc_workload:
+        ok, _k = parity_sample(w, out, host)
+        ok_sample = 1.0 if ok else 0.0
+    ok_all = gather_over_ranks(ok_sample, red_dev)
 
     if rank == 0:
-        traffic = None
+        traffic, traffic_src = None, None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
         if os.path.exists(tf):
             with open(tf) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                tj = json.load(f)
+            traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = (f"profiles/traffic_{args.workload}.json: builder's rocprofv3 PMC passes "
+                           f"({tj.get('source', 'see file')}), not measured in this run")
+        workload_name = {
+            "fixed": ("config4: " if world == 8 else "config2: ") +
+                     "2^20 x 1400 B datagrams per GPU, fixed stride 1400, device-resident" +
+                     (" (8M x 1400 B over 8 GPUs)" if world == 8 else ""),
+            "csr": "config3: 2^20 mixed-length datagrams (64..1400 B uniform) per GPU, CSR int64 offsets",
+            "filter": "config-3 batch as wire datagrams through lnl_inbound_filter_csr_dev",
+            "xor": "XOR layer over the config-2 batch, in place (22-byte key)",
+            "dispatch": "2^20 accepted MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire), "
+                        "lnl_dispatch_csr_dev"}[args.workload]
         line = {
             "metric": {"fixed": METRIC,
                        "csr": "CRC32C GB/s (device-resident) over 1M mixed-length (64-1400B) packets; bit-exact",
@@ -291,11 +427,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic (torch.randint on device, seed 42+rank), resident in HBM before timing",
             "config": {
-                "workload": {"fixed": "config2: 2^20 x 1400 B datagrams per GPU, fixed stride 1400, device-resident",
-                             "csr": "config3: 2^20 mixed-length datagrams (64..1400 B uniform) per GPU, CSR int64 offsets",
-                             "filter": "config-3 batch as wire datagrams through lnl_inbound_filter_csr_dev",
-                             "xor": "XOR layer over the config-2 batch, in place (22-byte key)",
-                             "dispatch": "2^20 accepted MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire), lnl_dispatch_csr_dev"}[args.workload],
+                "workload": workload_name,
                 "packets_per_gpu": w["n"],
                 "payload_bytes_per_gpu": w["payload"],
                 "parallelism": f"shard{world} (contiguous packet ranges, no data-path collectives)",
@@ -307,56 +439,54 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": w["algo"],
-                "kernel_ms": round(kern_ms, 5),
+                "kernel_ms": round(kern_max, 5),
+                "kernel_ms_per_rank": [round(k, 5) for k in kern_all],
             },
         }
+        if DRY:
+            line["dry_run"] = "LNL_BENCH_DRYRUN=1: CPU plumbing test, no kernel ran; figures are meaningless"
         if "line_bytes" in w:  # random narrow reads: HBM moves whole 64-B sectors
-            lb = w["line_bytes"] / (kern_ms * 1e-3) / 1e9
+            lb = w["line_bytes"] / (kern_max * 1e-3) / 1e9
             line["roofline"]["sector_granular_bytes_per_launch"] = w["line_bytes"]
             line["roofline"]["sector_granular_achieved"] = round(lb, 1)
             line["roofline"]["sector_granular_frac"] = round(lb / HBM_PEAK_GBS, 4)
-        probe = hbm_probe_peak(w["data"], device)
-        if probe:
-            line["roofline"]["measured_stream_read_peak_gbs"] = round(probe, 1)
-        if world == 1 and not args.no_cpu_baseline and not (w.get("xor") or w.get("filter") or w.get("dispatch")):
-            gpu_out = out.cpu().numpy().view(np.uint32)
-            res, threads, desc, exact = cpu_baseline(w, gpu_out)
+        if not DRY:
+            probe = hbm_probe_peak(w["data"], device)
+            if probe:
+                peak = max(probe.values())
+                line["roofline"]["measured_stream_read_peak_gbs"] = round(peak, 1)
+                line["roofline"]["measured_stream_read_forms_gbs"] = {
+                    "global_load_dwordx4 nt": round(probe[0], 1), "global_load_lds_dwordx4 nt": round(probe[1], 1)}
+                line["roofline"]["frac_of_measured_peak"] = round(achieved / peak, 4)
+        if crc_workload:
+            line["parity_on_sample"] = ("bit-exact" if min(ok_all) == 1.0 else "MISMATCH") + \
+                f" (first {min(w['n'], 1 << 14)} datagrams of each of {world} rank(s) vs the oracle)"
+        if world == 1 and crc_workload and not args.no_cpu_baseline:
+            res, cores, ref = cpu_baseline(w, host)
+            exact = bool(np.array_equal(out.cpu().numpy().view(np.uint32), ref))
             line["cpu_baseline"] = {
-                "value": round(res[threads][0], 3),
+                "value": round(res[cores], 3),
                 "unit": "GB/s",
-                "cores": threads,
+                "cores": cores,
                 "kind": "port",
-                "sample": desc + f"; oracle SSE4.2 crc32 loop, OpenMP {threads} threads, best of repeats over ~5 s",
-                "single_core_value": round(res[1][0], 3),
+                "sample": f"the whole batch ({w['n']} datagrams, {w['payload'] / 1e9:.3f} GB, copied to host "
+                          f"memory untimed); oracle SSE4.2 crc32 loop, OpenMP, median of repeats over ~2 s",
+                "single_core_value": round(res[1], 3),
+                "nproc": os.cpu_count(),
+                "cores_available": cores,
+                "cpu_model": cpu_model(),
             }
-            line["parity_on_sample"] = "bit-exact" if exact else "MISMATCH"
-        if args.host_path and world == 1:
-            line["host_path"] = host_path_rate(P, w)
+            line["parity_whole_batch"] = "bit-exact" if exact else "MISMATCH"
+        if world == 1 and crc_workload and not args.no_host_path:
+            hp, got = host_path_rate(P, host, w, torch.cuda.current_device())
+            hp["parity"] = "bit-exact vs the device-resident output" if np.array_equal(
+                got, out.cpu().numpy().view(np.uint32)) else "MISMATCH"
+            line["host_path"] = hp
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def host_path_rate(P, w):
-    """Config 5: host-resident pinned batch -> lnl_crc32c_batch_host (H2D +
-    kernel + D2H over 2 streams).  PCIe-inclusive; never the headline value."""
-    if w["off"] is None:
-        n, L = w["n"], w["L"]
-        host = w["data"].cpu().pin_memory()
-        off = np.arange(0, (n + 1) * L, L, dtype=np.uint64)
-    else:
-        host = w["data"].cpu().pin_memory()
-        off = w["off"].cpu().numpy().astype(np.uint64)
-    arr = host.numpy()
-    P.batch_host(arr, off, torch.cuda.current_device())
-    t0 = time.perf_counter()
-    reps = 3
-    for _ in range(reps):
-        P.batch_host(arr, off, torch.cuda.current_device())
-    dt = (time.perf_counter() - t0) / reps
-    return {"value": round(w["payload"] / dt / 1e9, 2), "unit": "GB/s",
-            "what": "pinned host batch, lnl_crc32c_batch_host, H2D+kernel+D2H, 2 streams"}
 
 
 if __name__ == "__main__":

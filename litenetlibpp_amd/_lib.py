@@ -83,9 +83,6 @@ def lib() -> ctypes.CDLL:
     L.lnl_crc32c_last_error.argtypes = []
     L.lnl_crc32c_abi_version.restype = ctypes.c_int
     L.lnl_crc32c_abi_version.argtypes = []
-    # experiment knob (not in include/lnl_crc32c.h): kernel of large CSR batches
-    L.lnl_crc32c_set_csr_path.restype = ctypes.c_int
-    L.lnl_crc32c_set_csr_path.argtypes = [ctypes.c_int]
     _lib = L
     return L
 

@@ -228,6 +228,9 @@ def dispatch(data, offsets, status, cap: Optional[int] = None, stream=None):
     _check_off(offsets, data)
     n = offsets.numel() - 1
     dev = data.device
+    if not (isinstance(status, torch.Tensor) and status.is_cuda and status.dtype == torch.uint8
+            and status.is_contiguous() and status.numel() >= max(n, 0) and status.device == dev):
+        raise TypeError("status must be a contiguous uint8 CUDA tensor of >= n entries on the data's device")
     total = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def run(c):
@@ -240,7 +243,7 @@ def dispatch(data, offsets, status, cap: Optional[int] = None, stream=None):
         return start, length, parent
 
     start, length, parent = run(cap if cap is not None else 0)
-    t = int(total.item())
+    t = int(total.item()) & 0xFFFFFFFF  # u32 count
     if cap is None:
         start, length, parent = run(t)
         cap = t
@@ -285,11 +288,31 @@ def xor_layer_fixed(data, stride: int, length: int, n: int, key, stream=None) ->
                                             _stream_handle(stream)), "lnl_xor_layer_fixed_dev")
 
 
+def _host_csr(data, offsets):
+    """Contiguous uint8 bytes and uint64 offsets of a host CSR batch, checked
+    the way the C ABI cannot (it never sees the buffer's size): offsets start
+    at >= 0, never decrease and end inside data.  A negative int64 offset
+    would otherwise wrap to a huge uint64 and the H2D copy read out of bounds."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(offsets)
+    if off.ndim != 1 or off.size == 0:
+        raise ValueError("offsets must be a 1-D array of n + 1 entries")
+    if off.dtype.kind not in "iu":
+        raise TypeError("offsets must be an integer array")
+    if off.dtype.kind == "i" and off.size and int(off.min()) < 0:
+        raise ValueError("negative offset")
+    off = off.astype(np.uint64, copy=False)
+    if off.size > 1 and bool((off[1:] < off[:-1]).any()):
+        raise ValueError("offsets decrease")
+    if int(off[-1]) > data.size:
+        raise ValueError(f"offsets end at {int(off[-1])}, past the {data.size}-byte buffer")
+    return data, off
+
+
 def inbound_filter_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
     """Host-resident burst through the GPU inbound filter (H2D -> filter ->
     D2H on 2 streams).  Blocking.  Returns uint8 status codes."""
-    data = np.ascontiguousarray(data, dtype=np.uint8)
-    offsets = np.ascontiguousarray(offsets).astype(np.uint64, copy=False)
+    data, offsets = _host_csr(data, offsets)
     n = offsets.size - 1
     out = np.empty(max(n, 0), dtype=np.uint8)
     if n > 0:
@@ -316,8 +339,7 @@ def ingress_recv_batch(fd: int, buf: np.ndarray, max_n: int, wait_ms: int = 0):
 def batch_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
     """Host-resident batch over the GPU (H2D -> kernel -> D2H on 2 streams).
     Blocking.  ``data`` uint8, ``offsets`` uint64/int64 with n+1 entries."""
-    data = np.ascontiguousarray(data, dtype=np.uint8)
-    offsets = np.ascontiguousarray(offsets).astype(np.uint64, copy=False)
+    data, offsets = _host_csr(data, offsets)
     n = offsets.size - 1
     out = np.empty(max(n, 0), dtype=np.uint32)
     if n > 0:
@@ -330,8 +352,7 @@ def batch_host_multi(data: np.ndarray, offsets: np.ndarray, devices) -> np.ndarr
     """Host-resident batch split over several GPUs (contiguous datagram ranges
     of ceil(n / len(devices)), one host thread per range, no data exchanged
     between devices).  Blocking.  Mirrors lnl_crc32c_batch_host_multi."""
-    data = np.ascontiguousarray(data, dtype=np.uint8)
-    offsets = np.ascontiguousarray(offsets).astype(np.uint64, copy=False)
+    data, offsets = _host_csr(data, offsets)
     devs = np.ascontiguousarray(list(devices), dtype=np.int32)
     if devs.size == 0:
         raise ValueError("empty device list")

@@ -26,6 +26,10 @@
 #include "crc32c_kernels.h"
 #include "crc32c_seg.h"
 
+#ifndef LNL_EXPERIMENTS
+#define LNL_EXPERIMENTS 0  // 1: the experiments build (tools/kvariants.py), never the product
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -156,9 +160,10 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
 #ifndef LNL_BUCKET_MIN_N
 #define LNL_BUCKET_MIN_N 16384
 #endif
-// CSR kernel selection.  The default is the bucketed batch kernel; the other
-// three are experiments kept for measurement (tools/kvariants.py) and covered
-// by the parity tests, which switch paths with lnl_crc32c_set_csr_path():
+// CSR kernel selection.  The product library has one path: the bucketed batch
+// kernel.  The experiments build (-DLNL_EXPERIMENTS=1, tools/kvariants.py,
+// build/variants/*.so -- never loaded by the product path) adds three more,
+// selected with lnl_crc32c_set_csr_path() or LNL_CSR_PATH:
 //   uniform  crc32c_csr.hip: uniform line-count batches, shared lines fetched
 //            once (786 MB instead of 968 MB per config-3 batch) -- but its
 //            kernel streams them slower and its plan + tail epilogue cost more:
@@ -169,6 +174,9 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
 // The initial value comes from the environment (LNL_CSR_PATH=bucketed |
 // uniform | seg | pairs).
 enum CsrPath : int { kPathBucketed = 0, kPathUniform = 1, kPathSeg = 2, kPathPairs = 3 };
+#if !LNL_EXPERIMENTS
+constexpr int csr_path() { return kPathBucketed; }
+#else
 std::atomic<int> g_csr_path{-1};
 int csr_path() {
     int p = g_csr_path.load(std::memory_order_relaxed);
@@ -298,9 +306,11 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
     if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
     return rc;
 }
+#endif  // LNL_EXPERIMENTS
 
 int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
     if (a.n < LNL_BUCKET_MIN_N) return launch(S, a, mode, st);
+#if LNL_EXPERIMENTS
     if (mode == lnl::kModeCsr) {
         switch (csr_path()) {
             case kPathUniform: return launch_csr_uniform(S, a, st);
@@ -309,6 +319,7 @@ int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st)
             default: break;
         }
     }
+#endif
     void* scratch = nullptr;
     const size_t bytes = lnl::bucket_scratch_words(a.n) * sizeof(uint32_t);
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
@@ -369,15 +380,18 @@ extern "C" const char* lnl_crc32c_last_error(void) { return g_err.c_str(); }
 
 extern "C" int lnl_crc32c_abi_version(void) { return LNL_CRC32C_ABI_VERSION; }
 
-// Experiment knob, not part of include/lnl_crc32c.h: selects the kernel of
-// large CSR / verify batches (0 bucketed batch kernel, 1 uniform, 2 segment,
-// 3 pair; see csr_path above).  Returns the previous path, or -EINVAL.
+#if LNL_EXPERIMENTS
+// Experiments build only (not in include/lnl_crc32c.h, not in the product
+// library): selects the kernel of large CSR / verify batches (0 bucketed batch
+// kernel, 1 uniform, 2 segment, 3 pair; see csr_path above).  Returns the
+// previous path, or -EINVAL.
 extern "C" int lnl_crc32c_set_csr_path(int path) {
     if (path < kPathBucketed || path > kPathPairs) return fail(-EINVAL, "CSR path %d out of range", path);
     const int prev = csr_path();
     g_csr_path.store(path);
     return prev;
 }
+#endif
 
 extern "C" int lnl_crc32c_batch_fixed_dev(const uint8_t* d_base, size_t stride, uint32_t len,
                                           uint32_t n, uint32_t* d_out, void* hip_stream) {
@@ -458,6 +472,9 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
     hipStream_t st = (hipStream_t)hip_stream;
     const int path = csr_path();
     if (n < LNL_BUCKET_MIN_N || path == kPathBucketed) return launch_csr(*S, a, lnl::kModeVerify, st);
+#if !LNL_EXPERIMENTS
+    return fail(-EINVAL, "unreachable CSR path %d", path);
+#else
     // large batches on an experiment path: CRCs of the whole wire datagrams
     // with that path's kernel, then ok / body CRC per datagram (crc32c_verify.hip)
     void* wire = nullptr;
@@ -484,6 +501,7 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
     e = hipFreeAsync(wire, st);
     if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
     return rc;
+#endif
 }
 }  // namespace
 
@@ -554,6 +572,12 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         S->cap_bytes = nb;
         S->cap_n = need_n;
     }
+    // after the first enqueue, every error path drains both streams first: the
+    // caller may free h_base / h_out as soon as we return
+    auto drained = [&](int rc) {
+        for (int s2 = 0; s2 < 2; ++s2) (void)hipStreamSynchronize(S->streams[s2]);
+        return rc;
+    };
     uint32_t i = 0;
     int k = 0;
     while (i < n) {
@@ -564,10 +588,10 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         hipStream_t st = S->streams[k];
         if (cb && (e = hipMemcpyAsync(S->d_bytes[k], h_base + h_off[i], cb, hipMemcpyHostToDevice, st)) !=
                       hipSuccess)
-            return hip_fail(e, "H2D bytes");
+            return drained(hip_fail(e, "H2D bytes"));
         if ((e = hipMemcpyAsync(S->d_off[k], h_off + i, (size_t)(cn + 1) * 8, hipMemcpyHostToDevice, st)) !=
             hipSuccess)
-            return hip_fail(e, "H2D offsets");
+            return drained(hip_fail(e, "H2D offsets"));
         lnl::BatchArgs a{};
         a.base = S->d_bytes[k];
         a.off = S->d_off[k];
@@ -577,19 +601,19 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         if (filter) {
             a.ok = (uint8_t*)S->d_out[k];
             a.filter = 1;
-            if (int rc = launch_csr(*S, a, lnl::kModeVerify, st)) return rc;
+            if (int rc = launch_csr(*S, a, lnl::kModeVerify, st)) return drained(rc);
         } else {
             a.out = S->d_out[k];
-            if (int rc = launch_csr(*S, a, lnl::kModeCsr, st)) return rc;
+            if (int rc = launch_csr(*S, a, lnl::kModeCsr, st)) return drained(rc);
         }
         if ((e = hipMemcpyAsync((uint8_t*)h_out + (size_t)i * esz, S->d_out[k], (size_t)cn * esz,
                                 hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return hip_fail(e, "D2H");
+            return drained(hip_fail(e, "D2H"));
         i = j;
         k ^= 1;
     }
     for (int s = 0; s < 2; ++s)
-        if ((e = hipStreamSynchronize(S->streams[s])) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        if ((e = hipStreamSynchronize(S->streams[s])) != hipSuccess) return drained(hip_fail(e, "hipStreamSynchronize"));
     return 0;
 }
 }  // namespace
@@ -617,6 +641,7 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     if (cap && (!d_pkt_start || !d_pkt_len || !d_pkt_parent)) return fail(-EINVAL, "NULL output");
     DeviceState* S;
     if (int rc = current_device(&S)) return rc;
+#if LNL_EXPERIMENTS
     // LNL_DISPATCH_ONEPASS=1: one launch with a decoupled look-back (experiment,
     // parity-clean but 0.61 ms against 0.18 for count + scan + emit)
     static const bool onepass = [] {
@@ -627,6 +652,10 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
         const char* e = getenv("LNL_DISPATCH_NT");
         return e && e[0] == '1' ? 1u : 0u;
     }();
+#else
+    constexpr bool onepass = false;   // product: count + scan + emit
+    constexpr uint32_t nt_stores = 0;  // plain stores (nt measured neutral)
+#endif
     if (onepass) {
         const size_t nwg = ((size_t)n + 255) / 256;
         void* flags = nullptr;
@@ -697,19 +726,26 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
     a.n = n;
     a.key_len = (uint32_t)key_len;
     memcpy(a.key, key, key_len);
-    // fixed stride, stride >= 16, 16-byte aligned: the flat kernel (whole pieces
-    // per lane, coalesced); LNL_XOR_FLAT=0 keeps the per-datagram kernel
+    // contiguous fixed stride (stride == len >= 16), 16-byte aligned: the flat
+    // kernel (whole pieces per lane, coalesced).  Strides with gaps take the
+    // per-datagram kernel, which never touches the gap bytes (the flat kernel
+    // would rewrite them unchanged -- a lost update for a concurrent writer).
+#if LNL_EXPERIMENTS
     static const int flat_v = [] {
-        const char* e = getenv("LNL_XOR_FLAT");
-        return e ? atoi(e) : 6;  // 2 pieces in flight, nontemporal
+        const char* e = getenv("LNL_XOR_FLAT");  // 0: per-datagram kernel
+        return e ? atoi(e) : 6;
     }();
     static const int flat_wg = [] {
         const char* e = getenv("LNL_XOR_FLAT_WG");  // workgroups per CU
         return e ? std::max(1, atoi(e)) : 8;
     }();
+#else
+    constexpr int flat_v = 6;   // 2 pieces in flight, nontemporal
+    constexpr int flat_wg = 8;  // workgroups per CU
+#endif
     const bool flat_on = flat_v > 0;
     const uint64_t span = d_off ? 0 : (uint64_t)(n - 1) * stride + len;
-    if (flat_on && !d_off && stride >= 16 && stride < (1u << 31) && len >= 1 &&
+    if (flat_on && !d_off && stride == len && stride >= 16 && stride < (1u << 31) && len >= 1 &&
         ((uintptr_t)d_base & 15u) == 0 && span < (1ull << 35)) {
         lnl::FlatArgs f{};
         f.span = span;

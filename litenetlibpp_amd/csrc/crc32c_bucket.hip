@@ -25,6 +25,10 @@
 
 #include "crc32c_kernels.h"
 
+#ifndef LNL_EXPERIMENTS
+#define LNL_EXPERIMENTS 0
+#endif
+
 namespace lnl {
 
 namespace {
@@ -44,10 +48,12 @@ namespace {
 #endif
 
 constexpr int kThreads = 256;
+#if LNL_EXPERIMENTS
 constexpr int kPerThread = 16;                    // pair count pass
 constexpr uint32_t kPerBlock = kThreads * kPerThread;
 constexpr int kScatterPerThread = 16;             // pair scatter pass
 constexpr uint32_t kScatterPerBlock = kThreads * kScatterPerThread;
+#endif
 constexpr int kBucketPerThread = 4;               // bucket count and scatter passes
 constexpr uint32_t kBucketPerBlock = kThreads * kBucketPerThread;
 
@@ -363,7 +369,8 @@ __global__ __launch_bounds__(kWinThreads) void bucket_window_kernel(BucketArgs a
 }
 static_assert(kBuckets == 64, "bucket_window_kernel scans the counts with one wave");
 
-// ---- pairs (crc32c_pair.hip) -----------------------------------------------
+#if LNL_EXPERIMENTS
+// ---- pairs (crc32c_pair.hip; experiments build only) ------------------------
 
 // Key of item j (kPairKeys: overflow) and, for the scatter, its descriptor.
 __device__ inline uint32_t pair_key(const PairPrepArgs& a, uint32_t j, uint4* d = nullptr) {
@@ -495,8 +502,10 @@ __global__ __launch_bounds__(kThreads) void pair_scatter_kernel(PairPrepArgs a) 
     }
 }
 
+#endif  // LNL_EXPERIMENTS
 }  // namespace
 
+#if LNL_EXPERIMENTS
 size_t pair_prep_scratch_words(uint32_t n) {
     const size_t items = ((size_t)n + 1) / 2;
     return (kPairKeys + 1) + kPairKeys + 4 + kPairKeys + 4 * (items + 64 * (size_t)kPairKeys) + ((size_t)n + 1) + 4;
@@ -527,15 +536,24 @@ hipError_t launch_pair_prep(const PairPrepArgs& a, hipStream_t stream) {
 
 
 
-// LNL_BUCKET_WINDOW=1..6: per-window sort (launch_csr_buckets lists the window
-// sizes and workgroup shapes); 0: the global bucket layout
+#endif  // LNL_EXPERIMENTS
+
+// Descriptor layout of the product build: windows of 2048 datagrams sorted by
+// line count, 256-thread workgroups, placed in 4 sweeps.  The
+// experiments build (tools/kvariants.py, -DLNL_EXPERIMENTS=1) reads
+// LNL_BUCKET_WINDOW=0..6 / LNL_BUCKET_SPREAD / LNL_BUCKET_XCD to select the
+// measured alternatives; the product library never reads the environment.
 int bucket_window() {
+#if LNL_EXPERIMENTS
     static const int w = [] {
         const char* e = getenv("LNL_BUCKET_WINDOW");
         if (!e) return 1;  // default: windows of 2048
         return e[0] >= '1' && e[0] <= '6' ? e[0] - '0' : 0;
     }();
     return w;
+#else
+    return 1;
+#endif
 }
 
 size_t bucket_scratch_words(uint32_t n) {
@@ -576,8 +594,10 @@ hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream) {
         const dim3 g((a.n + W - 1) / W);
         BucketArgs b = a;
         b.spread = 4u;
+#if LNL_EXPERIMENTS
         if (const char* e = getenv("LNL_BUCKET_SPREAD")) b.spread = (uint32_t)atoi(e);
         if (const char* e = getenv("LNL_BUCKET_XCD")) b.xcd = (uint32_t)atoi(e);
+#endif
         switch (wv) {
             case 2: hipLaunchKernelGGL((bucket_window_kernel<8>), g, dim3(512), 0, stream, b); break;
             case 3: hipLaunchKernelGGL((bucket_window_kernel<16>), g, dim3(512), 0, stream, b); break;

@@ -37,6 +37,10 @@
 #include "crc32c_kernels.h"
 #include "lnl_packet.h"
 
+#ifndef LNL_EXPERIMENTS
+#define LNL_EXPERIMENTS 0
+#endif
+
 namespace lnl {
 
 namespace {
@@ -179,7 +183,8 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
     }
 }
 
-// One pass (experiment, LNL_DISPATCH_ONEPASS=1): walk, count and write in one launch.  The workgroup's
+#if LNL_EXPERIMENTS
+// One pass (experiments build only, LNL_DISPATCH_ONEPASS=1): walk, count and write in one launch.  The workgroup's
 // packet offset comes from a decoupled look-back over per-workgroup flags
 // (a.look[b] = flag << 32 | value; flag 1: this workgroup's own count,
 // 2: inclusive prefix), so there is no device-wide scan launch and the
@@ -327,6 +332,8 @@ __global__ __launch_bounds__(256) void dispatch_onepass_kernel(DispatchArgs a) {
     }
 }
 
+#endif  // LNL_EXPERIMENTS
+
 }  // namespace
 
 size_t dispatch_scan_bytes(uint32_t n) {
@@ -339,10 +346,14 @@ size_t dispatch_scan_bytes(uint32_t n) {
 
 hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream) {
     const dim3 grid((a.n + 255u) / 256u);
+#if LNL_EXPERIMENTS
     if (a.look) {  // one pass (flags zeroed by the caller)
         hipLaunchKernelGGL(dispatch_onepass_kernel, grid, dim3(256), 0, stream, a);
         return hipGetLastError();
     }
+#else
+    if (a.look) return hipErrorInvalidValue;  // the one-pass form is not in the product build
+#endif
     hipLaunchKernelGGL(dispatch_count_kernel, grid, dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -33,6 +33,10 @@
 
 #include "crc32c_kernels.h"
 
+#ifndef LNL_EXPERIMENTS
+#define LNL_EXPERIMENTS 0
+#endif
+
 namespace lnl {
 
 namespace {
@@ -256,7 +260,11 @@ __global__ __launch_bounds__(kThreads) void xor_flat_kernel(XorArgs a, FlatArgs 
 }  // namespace
 
 hipError_t launch_xor_flat(const XorArgs& a, const FlatArgs& f, int grid, int variant, hipStream_t stream) {
-    switch (variant) {  // pieces in flight per lane x cache policy (measured in DESIGN 5)
+#if !LNL_EXPERIMENTS
+    (void)variant;  // product: 2 pieces in flight per lane, nontemporal
+    hipLaunchKernelGGL((xor_flat_kernel<2, true>), dim3(grid), dim3(kThreads), 0, stream, a, f);
+#else
+    switch (variant) {  // pieces in flight per lane x cache policy (measured in DESIGN 4.8)
         case 2: hipLaunchKernelGGL((xor_flat_kernel<4, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
         case 3: hipLaunchKernelGGL((xor_flat_kernel<8, false>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
         case 4: hipLaunchKernelGGL((xor_flat_kernel<8, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
@@ -264,6 +272,7 @@ hipError_t launch_xor_flat(const XorArgs& a, const FlatArgs& f, int grid, int va
         case 6: hipLaunchKernelGGL((xor_flat_kernel<2, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
         default: hipLaunchKernelGGL((xor_flat_kernel<4, false>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
     }
+#endif
     return hipGetLastError();
 }
 

@@ -29,6 +29,18 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(value: float, device=None) -> list[float]:
+    """Every rank's scalar, in rank order (reporting only)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(value)]
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [float(p.item()) for p in parts]
+
+
 def sum_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist

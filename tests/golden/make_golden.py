@@ -46,8 +46,13 @@ KAT = [
 
 def main():
     rng = np.random.default_rng(20261015)
-    with open(os.path.join(HERE, "kat.json"), "w") as f:
-        json.dump(KAT, f, indent=1)
+    path = os.path.join(HERE, "kat.json")
+    keep = []
+    if os.path.exists(path):  # recipe pins are written by make_recipe_pins.py
+        with open(path) as f:
+            keep = [k for k in json.load(f) if "recipe" in k]
+    with open(path, "w") as f:
+        json.dump(KAT + keep, f, indent=1)
 
     # CSR fixture: contiguous datagrams of the edge lengths x {zeros, 0xFF,
     # random} plus random lengths; starts therefore fall on every alignment.

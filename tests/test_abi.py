@@ -110,3 +110,33 @@ def test_batch_entry_points_refuse_without_gpu(pkg):
     assert list(out) == [0, 0, 0, 0]
     assert L.lnl_crc32c_batch_host_multi(ctypes.addressof(buf), ctypes.addressof(off), 4, ctypes.addressof(out),
                                          None, 0) == -22
+
+
+def test_product_library_has_no_experiment_knobs(pkg):
+    """The product .so has one kernel path per layout: no run-time path
+    selection and no LNL_* environment knobs (those live in the experiments
+    build, tools/kvariants.py -> build/variants/*.so)."""
+    import subprocess
+    from litenetlibpp_amd._lib import LIB_PATH
+    blob = open(LIB_PATH, "rb").read()
+    for knob in (b"LNL_CSR_PATH", b"LNL_BUCKET_WINDOW", b"LNL_BUCKET_SPREAD", b"LNL_BUCKET_XCD",
+                 b"LNL_DISPATCH_ONEPASS", b"LNL_DISPATCH_NT", b"LNL_XOR_FLAT"):
+        assert knob not in blob, knob
+    exported = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True,
+                              check=True).stdout
+    assert "lnl_crc32c_set_csr_path" not in exported
+
+
+def test_host_batch_offsets_checked_before_the_call(pkg):
+    """The host entry points never see the buffer's size, so the wrappers check
+    the offsets first: out of range, decreasing or negative offsets raise
+    before any copy (a negative int64 wrapped to a huge uint64)."""
+    import numpy as np
+    import pytest
+    data = np.zeros(100, np.uint8)
+    for off in (np.array([0, 50, 101], np.uint64), np.array([0, 60, 50], np.int64),
+                np.array([-8, 10], np.int64)):
+        for fn in (lambda o: pkg.batch_host(data, o, 0), lambda o: pkg.inbound_filter_host(data, o, 0),
+                   lambda o: pkg.batch_host_multi(data, o, [0])):
+            with pytest.raises(ValueError):
+                fn(off)

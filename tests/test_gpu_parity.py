@@ -32,20 +32,10 @@ def P():
     return pkg
 
 
-# Large CSR / verify batches (>= 16 Ki datagrams) have four kernel paths in the
-# library (crc32c_api.cpp, csr_path): the default bucketed batch kernel and three
-# experiments.  The large-batch tests run on every path.
-CSR_PATHS = {"bucketed": 0, "uniform": 1, "seg": 2, "pairs": 3}
-all_paths = pytest.mark.parametrize("csr_path", list(CSR_PATHS), indirect=True)
-
-
-@pytest.fixture
-def csr_path(P, request):
-    L = P.lib()
-    prev = L.lnl_crc32c_set_csr_path(CSR_PATHS[request.param])
-    assert prev >= 0
-    yield request.param
-    L.lnl_crc32c_set_csr_path(prev)
+# Large CSR / verify batches (>= 16 Ki datagrams) take the product's large-batch
+# path (crc32c_api.cpp, launch_csr); the shapes below were written against the
+# experiment kernels too (pairs, segments, uniform batches: tools/kvariants.py)
+# and stay as edge cases for whichever kernel is the product's.
 
 
 def u32(t):
@@ -165,8 +155,7 @@ def test_csr_mixed_length_config3_shape(P):
     assert np.array_equal(got, exp)
 
 
-@all_paths
-def test_csr_bucketed_mix(P, csr_path):
+def test_csr_bucketed_mix(P):
     """Batches large enough for the line-count bucketing pre-pass
     (crc32c_bucket.hip): empty, 1..3-byte, line-crossing and very long
     datagrams (line-count bucket 63) mixed, buffer not line-aligned."""
@@ -187,8 +176,7 @@ def test_csr_bucketed_mix(P, csr_path):
 
 
 @pytest.mark.parametrize("case", ["odd_n", "tiny", "line_multiples", "overflow_heavy"])
-@all_paths
-def test_csr_pairs(P, csr_path, case):
+def test_csr_pairs(P, case):
     """CSR pair kernel (crc32c_pair.hip): a lone last datagram (odd n), pairs of
     tiny datagrams sharing one line, lengths that end exactly on line
     boundaries (unshared pairs), and many pairs too long for the pair buckets
@@ -214,8 +202,7 @@ def test_csr_pairs(P, csr_path, case):
 
 
 @pytest.mark.parametrize("case", ["segment_multiples", "line_multiples", "lead_and_tail", "tiny_excess"])
-@all_paths
-def test_csr_segments(P, csr_path, case):
+def test_csr_segments(P, case):
     """Shapes aimed at the CSR segment kernel (crc32c_seg.hip): datagram ends on segment boundaries (lengths of 2 KiB multiples, the
     segment size of batches this small), on line boundaries, a batch that
     starts and ends mid-line, and segments with more ends than a lane tracks
@@ -239,8 +226,7 @@ def test_csr_segments(P, csr_path, case):
     assert bad.size == 0, f"{case}: {bad.size} mismatches, first at {bad[:5]}"
 
 
-@all_paths
-def test_csr_segments_several_batches_per_wave(P, csr_path):
+def test_csr_segments_several_batches_per_wave(P):
     """A batch larger than one segment per lane at the largest segment size
     (> 2 GiB on 256 CUs): waves take several wave-batches."""
     rng = np.random.default_rng(600)
@@ -256,8 +242,7 @@ def test_csr_segments_several_batches_per_wave(P, csr_path):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
 
 
-@all_paths
-def test_csr_pairs_many_batches_per_wave(P, csr_path):
+def test_csr_pairs_many_batches_per_wave(P):
     """Far more pair batches than resident waves (persistent waves change
     batch many times: descriptor slots, next-batch prefetch), small data."""
     rng = np.random.default_rng(404)
@@ -271,8 +256,7 @@ def test_csr_pairs_many_batches_per_wave(P, csr_path):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
 
 
-@all_paths
-def test_verify_mode_bucketed(P, csr_path):
+def test_verify_mode_bucketed(P):
     rng = np.random.default_rng(22)
     n = 30000
     lens = rng.integers(0, 1433, n)
@@ -327,8 +311,7 @@ def _wire_batch(rng, n, corrupt_frac=0.2):
 
 
 @pytest.mark.parametrize("n", [1000, 40000])
-@all_paths
-def test_inbound_filter(P, csr_path, n):
+def test_inbound_filter(P, n):
     """lnl_inbound_filter_csr_dev: CRC layer, then net_packet::verify() of the
     stripped packet (reference-pinned restatement, tests/test_packet_verify.py),
     per datagram, on every CSR path (n = 1000 takes the unbucketed kernel)."""
@@ -341,8 +324,7 @@ def test_inbound_filter(P, csr_path, n):
     assert set(np.unique(exp)) == {0, 1, 2}
 
 
-@all_paths
-def test_full_config3_bit_exact(P, csr_path):
+def test_full_config3_bit_exact(P):
     # BASELINE config 3 at full size: 2^20 datagrams of 64..1400 B, CSR
     rng = np.random.default_rng(43)
     lens = 64 + rng.integers(0, 1337, 1 << 20)
@@ -688,6 +670,10 @@ def test_full_config2_survey_input(P):
     host = oracle.mt19937_64_bytes(42, n * L)
     got = u32(P.batch_fixed(dev(host), L, L, n))
     assert got[0] == 0xD26C5CFE
+    import json
+    with open(os.path.join(GOLD, "kat.json")) as f:
+        pin = {k["recipe"]: k for k in json.load(f) if "recipe" in k}["config2"]
+    assert int(np.bitwise_xor.reduce(got)) == pin["xor_all"]   # checksum of checksums
     exp = oracle.batch_fixed(host, L, L, n)
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
@@ -699,3 +685,27 @@ def test_error_paths_raise(P):
         P.batch_fixed(data, 100, 100, 2)
     with pytest.raises(TypeError):
         P.batch_fixed(data.cpu(), 10, 10, 1)
+
+
+def test_full_config3_survey_recipe(P):
+    """SURVEY.md 8(d) config 3 recipe at full size: L_i = 64 + (u_i mod 1337),
+    u = mt19937_64(43), bytes mt19937_64(44), packed CSR; out[0] and the XOR of
+    all CRCs equal the pins in tests/golden/kat.json (make_recipe_pins.py), and
+    every CRC equals the oracle's."""
+    import ctypes
+    import json
+    with open(os.path.join(GOLD, "kat.json")) as f:
+        pin = {k["recipe"]: k for k in json.load(f) if "recipe" in k}["config3"]
+    n = 1 << 20
+    u = np.empty(n, np.uint64)
+    L = oracle.load()
+    L.oracle_fill_mt19937_64.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]
+    L.oracle_fill_mt19937_64(43, u.ctypes.data, n)
+    off = np.concatenate([[0], np.cumsum(np.uint64(64) + u % np.uint64(1337))]).astype(np.uint64)
+    host = oracle.mt19937_64_bytes(44, int(off[-1]))
+    got = u32(P.batch_csr(dev(host), dev(off.view(np.int64), torch.int64)))
+    assert int(got[0]) == pin["out0"]
+    assert int(np.bitwise_xor.reduce(got)) == pin["xor_all"]
+    exp = oracle.batch_csr(host, off)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"

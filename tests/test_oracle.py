@@ -18,7 +18,12 @@ KINDS = ["bitwise", "sliced", "hw"]
 
 def kats():
     with open(os.path.join(GOLD, "kat.json")) as f:
-        return json.load(f)
+        return [k for k in json.load(f) if "hex" in k]
+
+
+def recipe_pins():
+    with open(os.path.join(GOLD, "kat.json")) as f:
+        return {k["recipe"]: k for k in json.load(f) if "recipe" in k}
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -90,3 +95,20 @@ def test_survey_config2_pin():
     assert oracle.crc(b[:1400], "bitwise") == 0xD26C5CFE
     assert oracle.crc(b[:1400], "sliced") == 0xD26C5CFE
 
+
+
+def test_survey_config3_recipe_pin():
+    """L_0 = 64 + (mt19937_64(43)[0] mod 1337) and the
+    first datagram is the first L_0 bytes of mt19937_64(44); its CRC is the
+    pin tests/golden/make_recipe_pins.py recorded (full batch: -m gpu)."""
+    import ctypes
+    pin = recipe_pins()["config3"]
+    L = oracle.load()
+    L.oracle_fill_mt19937_64.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]
+    u = np.empty(1, np.uint64)
+    L.oracle_fill_mt19937_64(43, u.ctypes.data, 1)
+    l0 = 64 + int(u[0]) % 1337
+    b = oracle.mt19937_64_bytes(44, l0)
+    for kind in KINDS:
+        assert oracle.crc(b, kind) == pin["out0"]
+    assert recipe_pins()["config2"]["out0"] == 0xD26C5CFE

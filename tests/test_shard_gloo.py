@@ -1,7 +1,8 @@
 """N > 1 path on the CPU: world_size-2 gloo.  Each rank checksums its own
-contiguous shard (with the oracle standing in for the GPU kernel -- this
-tests the partition and the timing reductions, not the kernel), and the
-shards reassemble to the single-process answer."""
+contiguous shard with the product's per-datagram CPU entry point
+(lnl_crc32c; the batch kernels need a GPU -- bench.py's spawn path is
+covered by tests/test_bench_spawn.py), and the shards reassemble to the
+oracle's single-process answer (the oracle is only the checker here)."""
 import os
 import socket
 
@@ -36,17 +37,18 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    import oracle
+    import litenetlibpp_amd as P
     n, L = 1000, 1400
     rng = np.random.default_rng(5)
     data = rng.integers(0, 256, n * L, dtype=np.uint8)   # every rank can regenerate the job's data
     s, c = shard_range(n, rank, world)
-    mine = oracle.batch_fixed(data[s * L:(s + c) * L], L, L, c)
+    mine = np.array([P.crc32c(data[(s + i) * L:(s + i + 1) * L]) for i in range(c)], dtype=np.uint32)
     parts = [None] * world
     dist.all_gather_object(parts, (s, mine.tolist()))
     t = max_over_ranks(1.0 + rank)
     b = sum_over_ranks(c * L)
     if rank == 0:
+        import oracle
         full = np.zeros(n, np.uint32)
         for st, vals in parts:
             full[st:st + len(vals)] = vals

@@ -11,7 +11,7 @@ WL=${2:-fixed}
 OUT=gpurun_out/prof_${TAG}_${WL}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python3 bench.py --workload $WL --steps 20 --warmup 5 --no-cpu-baseline"
+B="python3 bench.py --workload $WL --steps 20 --warmup 5 --no-cpu-baseline --no-host-path"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format rocpd csv -d "$OUT/trace" -o t -- $B > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o f -- $B > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o w -- $B > "$OUT/write.log" 2>&1

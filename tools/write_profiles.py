@@ -34,7 +34,7 @@ def main():
     shutil.copy(os.path.join(src, "trace", "t_kernel_stats.csv"),
                 os.path.join(dst, f"{tag}_{wl}_kernel_stats.csv"))
     md = [f"# {tag} {wl}: rocprofv3 summaries of `python3 bench.py --workload {wl} --steps 20 --warmup 5 "
-          f"--no-cpu-baseline`\n",
+          f"--no-cpu-baseline --no-host-path`\n",
           "Produced by `tools/profile_round.sh` on one MI355X; each section is a separate rocprofv3 run "
           "(kernel trace; then one PMC pass per counter group).\n"]
     # HBM bytes per API call: every product kernel the call launches (the CRC
