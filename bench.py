@@ -198,8 +198,12 @@ def launch(P, w, out, stream):
 
 # ------------------------------------------------------------------ context figures
 def hbm_probe_peak(data, device):
-    """Measured read-only streaming rate over the same buffer (context for the
-    nameplate peak): the best of the probe's forms (litenetlibpp_amd/csrc/hbm_probe.hip)."""
+    """Measured read-only streaming rates over the same buffer (context for
+    the nameplate peak; litenetlibpp_amd/csrc/hbm_probe.hip): forms 0 / 1 are
+    plain streams (global_load_dwordx4 nt, LDS-DMA nt) over the whole buffer;
+    forms 2-4 read it in the shape of a segment-per-lane CSR kernel (48-line
+    segments, one round of every resident wave: per-lane lines into VGPRs with
+    the default / nt policy, and by LDS-DMA)."""
     so = os.path.join(ROOT, "litenetlibpp_amd", "libhbm_probe.so")
     if not os.path.exists(so):
         return None
@@ -209,9 +213,13 @@ def hbm_probe_peak(data, device):
     L.lnl_probe_stream_read.restype = ctypes.c_int
     sink = torch.zeros(4, dtype=torch.int32, device=device)
     s = torch.cuda.current_stream()
-    nbytes = data.numel() // 1024 * 1024
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    seg_round = cus * 8 * 64 * 48 * 128
     best = {}
-    for form in (0, 1):
+    for form in (0, 1, 2, 3, 4):
+        nbytes = data.numel() // 8192 * 8192 if form < 2 else seg_round
+        if nbytes > data.numel() or nbytes == 0:
+            continue
         for _ in range(3):
             L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream, form)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -223,6 +231,30 @@ def hbm_probe_peak(data, device):
         torch.cuda.synchronize()
         best[form] = nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
     return best
+
+
+def cpu_quota() -> int | None:
+    """CPUs the cgroup grants this process (cpu.max quota / period), if capped.
+    On the GPU box os.cpu_count() and the affinity mask show the whole machine
+    while the job's share is a quota; threads beyond it only time-slice."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, p = f.read().split()[:2]
+            if q != "max":
+                return max(1, int(int(q) // int(p)))
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        if q > 0:
+            return max(1, q // p)
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def cpu_model() -> str:
@@ -258,6 +290,9 @@ def cpu_baseline(w, host):
         def run(th):
             return oracle.batch_csr(data, off, threads=th)
     cores = len(os.sched_getaffinity(0))
+    quota = cpu_quota()
+    if quota:
+        cores = min(cores, quota)
     res, ref = {}, None
     for th in (1, cores):
         times = []
@@ -269,7 +304,7 @@ def cpu_baseline(w, host):
             if time.perf_counter() > t_end and len(times) >= 3:
                 break
         res[th] = w["payload"] / float(np.median(times)) / 1e9
-    return res, cores, ref
+    return res, cores, ref, quota
 
 
 def parity_sample(w, out, host):
@@ -376,7 +411,7 @@ def main():
     end = max_over_ranks(t1, red_dev)       # the last rank's finish
     ms_per_step = (end - start) / args.steps * 1e3
     total_payload = sum_over_ranks(w["payload"], red_dev)
-    value = total_payload / ((end - start) or 1e-9) / 1e9
+    value = total_payload * args.steps / ((end - start) or 1e-9) / 1e9
     kern_all = gather_over_ranks(kern_ms, red_dev)
     kern_max = max(kern_all)
     achieved = w["algo"] / (kern_max * 1e-3) / 1e9
@@ -455,16 +490,18 @@ def main():
         if not DRY:
             probe = hbm_probe_peak(w["data"], device)
             if probe:
-                peak = max(probe.values())
+                peak = max(probe[0], probe[1])
+                names = {0: "global_load_dwordx4 nt", 1: "global_load_lds_dwordx4 nt",
+                         2: "segment lanes, VGPR loads", 3: "segment lanes, VGPR loads nt",
+                         4: "segment lanes, LDS-DMA nt"}
                 line["roofline"]["measured_stream_read_peak_gbs"] = round(peak, 1)
-                line["roofline"]["measured_stream_read_forms_gbs"] = {
-                    "global_load_dwordx4 nt": round(probe[0], 1), "global_load_lds_dwordx4 nt": round(probe[1], 1)}
+                line["roofline"]["measured_stream_read_forms_gbs"] = {names[k]: round(v, 1) for k, v in probe.items()}
                 line["roofline"]["frac_of_measured_peak"] = round(achieved / peak, 4)
         if crc_workload:
             line["parity_on_sample"] = ("bit-exact" if min(ok_all) == 1.0 else "MISMATCH") + \
                 f" (first {min(w['n'], 1 << 14)} datagrams of each of {world} rank(s) vs the oracle)"
         if world == 1 and crc_workload and not args.no_cpu_baseline:
-            res, cores, ref = cpu_baseline(w, host)
+            res, cores, ref, quota = cpu_baseline(w, host)
             exact = bool(np.array_equal(out.cpu().numpy().view(np.uint32), ref))
             line["cpu_baseline"] = {
                 "value": round(res[cores], 3),
@@ -475,7 +512,11 @@ def main():
                           f"memory untimed); oracle SSE4.2 crc32 loop, OpenMP, median of repeats over ~2 s",
                 "single_core_value": round(res[1], 3),
                 "nproc": os.cpu_count(),
-                "cores_available": cores,
+                "affinity_cpus": len(os.sched_getaffinity(0)),
+                "cgroup_cpu_quota": quota,
+                "cores_note": "threads = the CPUs this job may use: the affinity mask, capped by the cgroup "
+                              "cpu.max quota when there is one (on the GPU box nproc shows the whole machine "
+                              "but the job's share is a quota; more threads than that only time-slice)",
                 "cpu_model": cpu_model(),
             }
             line["parity_whole_batch"] = "bit-exact" if exact else "MISMATCH"

@@ -49,12 +49,110 @@ __global__ __launch_bounds__(256) void stream_read_lds(const uint8_t* __restrict
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// forms 2-4: the access shape of a segment-per-lane CSR kernel.  Lane l of
+// wave-batch w owns the R = kSegR consecutive 128-byte lines starting at
+// line (64 w + l) R and reads one line per step:
+//   form 2 / 3: each lane loads its own line into VGPRs (8 x dwordx4, 64
+//               different lines per wave-instruction), two lines in flight,
+//               default / nt cache policy
+//   form 4:     LDS-DMA, glds i fetches piece (lane & 7) of the line of lane
+//               8 i + lane / 8 (8 lines per wave-instruction), two rows of
+//               the wave in flight, then each lane reads its row back with
+//               8 x ds_read_b128 (the CRC kernels' load path)
+constexpr uint32_t kSegR = 48;
+
+template <bool kNT>
+__device__ inline void load_line(const u32x4* q, u32x4* v) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = kNT ? __builtin_nontemporal_load(q + k) : q[k];
+}
+
+template <bool kNT>
+__global__ __launch_bounds__(256) void seg_read_vgpr(const uint8_t* __restrict__ p, uint32_t nseg,
+                                                     uint32_t* __restrict__ sink) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
+    uint32_t acc = 0;
+    for (uint32_t wb = gw; wb * 64u < nseg; wb += nw) {
+        const uint32_t g = wb * 64u + lane;
+        const u32x4* q = (const u32x4*)(p + (size_t)(g < nseg ? g : nseg - 1u) * kSegR * 128u);
+        u32x4 a[8], b[8];
+        load_line<kNT>(q, a);
+        load_line<kNT>(q + 8, b);
+        for (uint32_t t = 0; t < kSegR; t += 2) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc ^= a[k].x ^ a[k].y ^ a[k].z ^ a[k].w;
+            if (t + 2 < kSegR) load_line<kNT>(q + 8 * (t + 2), a);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc ^= b[k].x ^ b[k].y ^ b[k].z ^ b[k].w;
+            if (t + 3 < kSegR) load_line<kNT>(q + 8 * (t + 3), b);
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void seg_read_lds(const uint8_t* __restrict__ p, uint32_t nseg,
+                                                    uint32_t* __restrict__ sink) {
+    __shared__ __attribute__((aligned(16))) uint4 lds[4 * 2 * 512];  // 2 x 8 KiB per wave
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t gw = blockIdx.x * 4u + wave, nw = gridDim.x * 4u;
+    uint4* const buf = lds + wave * 1024;
+    const uint32_t sub = lane >> 3, piece = lane & 7u;
+    uint32_t acc = 0;
+    for (uint32_t wb = gw; wb * 64u < nseg; wb += nw) {
+        const uint8_t* base = p + (size_t)wb * 64u * kSegR * 128u;
+        const uint32_t last = nseg - 1u - wb * 64u;  // lanes past the batch end re-read its last segment
+#define ISSUE(T, B)                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                   \
+        const uint32_t q = 8u * i + sub;                                                              \
+        const uint32_t qq = q < last ? q : last;                                                      \
+        __builtin_amdgcn_global_load_lds((const void*)(base + ((size_t)qq * kSegR + (T)) * 128u + 16u * piece), \
+                                         (void*)((B) + 64 * i), 16, 0, 2);                            \
+    }
+        ISSUE(0u, buf);
+        ISSUE(1u, buf + 512);
+        for (uint32_t t = 0; t < kSegR; ++t) {
+            uint4* const b = buf + (t & 1u) * 512;
+            if (t + 1 < kSegR)
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t ra = (uint32_t)(uintptr_t)(b + lane * 8);
+            uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+            asm volatile(
+                "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:16\n\tds_read_b128 %2, %8 offset:32\n\t"
+                "ds_read_b128 %3, %8 offset:48\n\tds_read_b128 %4, %8 offset:64\n\tds_read_b128 %5, %8 offset:80\n\t"
+                "ds_read_b128 %6, %8 offset:96\n\tds_read_b128 %7, %8 offset:112\n\ts_waitcnt lgkmcnt(0)"
+                : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(v4), "=&v"(v5), "=&v"(v6), "=&v"(v7)
+                : "v"(ra) : "memory");
+            acc ^= v0.x ^ v1.y ^ v2.z ^ v3.w ^ v4.x ^ v5.y ^ v6.z ^ v7.w;
+            if (t + 2 < kSegR) { ISSUE(t + 2u, b); }
+        }
+#undef ISSUE
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 extern "C" int lnl_probe_stream_read(const void* d, size_t bytes, uint32_t* d_sink, void* stream, int form) {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int grid = cus * 2;
-    if (form == 1) {
+    if (form >= 2 && form <= 4) {
+        const size_t nseg = bytes / (kSegR * 128u);
+        if (nseg == 0 || nseg > 0xFFFFFFFFull) return -22;
+        const uint32_t ns = (uint32_t)nseg;
+        if (form == 4)
+            hipLaunchKernelGGL(seg_read_lds, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d, ns,
+                               d_sink);
+        else if (form == 3)
+            hipLaunchKernelGGL(seg_read_vgpr<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                               (const uint8_t*)d, ns, d_sink);
+        else
+            hipLaunchKernelGGL(seg_read_vgpr<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                               (const uint8_t*)d, ns, d_sink);
+    } else if (form == 1) {
         const size_t chunks = bytes / 8192u;
         if (chunks == 0 || chunks > 0xFFFFFFFFull) return -22;
         hipLaunchKernelGGL(stream_read_lds, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d,
