@@ -216,8 +216,9 @@ def hbm_probe_peak(data, device):
     cus = torch.cuda.get_device_properties(device).multi_processor_count
     seg_round = cus * 8 * 64 * 48 * 128
     best = {}
-    for form in (0, 1, 2, 3, 4):
-        nbytes = data.numel() // 8192 * 8192 if form < 2 else seg_round
+    waves = {5: 5, 6: 6}
+    for form in (0, 1, 2, 3, 4, 5, 6, 7):
+        nbytes = data.numel() // 8192 * 8192 if form < 2 else seg_round * waves.get(form, 8) // 8
         if nbytes > data.numel() or nbytes == 0:
             continue
         for _ in range(3):
@@ -493,7 +494,9 @@ def main():
                 peak = max(probe[0], probe[1])
                 names = {0: "global_load_dwordx4 nt", 1: "global_load_lds_dwordx4 nt",
                          2: "segment lanes, VGPR loads", 3: "segment lanes, VGPR loads nt",
-                         4: "segment lanes, LDS-DMA nt"}
+                         4: "segment lanes, LDS-DMA nt", 5: "segment lanes, LDS-DMA nt, 5 waves/CU",
+                         6: "segment lanes, LDS-DMA nt, 6 waves/CU",
+                         7: "segment lanes, VGPR-staged nt + LDS transpose"}
                 line["roofline"]["measured_stream_read_peak_gbs"] = round(peak, 1)
                 line["roofline"]["measured_stream_read_forms_gbs"] = {names[k]: round(v, 1) for k, v in probe.items()}
                 line["roofline"]["frac_of_measured_peak"] = round(achieved / peak, 4)

@@ -25,6 +25,7 @@
 #include "crc32c_bitslice.h"
 #include "crc32c_kernels.h"
 #include "crc32c_seg.h"
+#include "crc32c_span.h"
 
 #ifndef LNL_EXPERIMENTS
 #define LNL_EXPERIMENTS 0  // 1: the experiments build (tools/kvariants.py), never the product
@@ -58,6 +59,7 @@ struct DeviceState {
     uint8_t* dummy = nullptr;  // 256 zero bytes of device memory
     uint32_t* fold = nullptr;  // kernel tables (lnl_build_tables), 12.5 KiB
     uint32_t* pow = nullptr;   // segment kernel's row-power tables (lnl_build_seg_tables), 3.5 KiB
+    uint32_t* span_tab = nullptr;  // span kernel's tables (lnl_build_span_tables), 20.5 KiB
     int cus = 0;
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)
@@ -94,10 +96,12 @@ int device_state(int dev, DeviceState** out) {
         (void)hipSetDevice(dev);
         static uint32_t host_fold[LNL_TABLE_WORDS];
         static uint32_t host_pow[lnl::kSegPowTables * 128];
+        static uint32_t host_span[lnl::kSpanTabWords];
         static std::once_flag fold_once;
         std::call_once(fold_once, [] {
             lnl_build_tables(host_fold);
             lnl_build_seg_tables(host_pow, (int)lnl::kSegPowTables);
+            lnl::lnl_build_span_tables(host_span);
         });
         e = hipMalloc(&S.dummy, 256);
         if (e == hipSuccess) e = hipMemset(S.dummy, 0, 256);
@@ -105,6 +109,8 @@ int device_state(int dev, DeviceState** out) {
         if (e == hipSuccess) e = hipMemcpy(S.fold, host_fold, sizeof host_fold, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&S.pow, sizeof host_pow);
         if (e == hipSuccess) e = hipMemcpy(S.pow, host_pow, sizeof host_pow, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc(&S.span_tab, sizeof host_span);
+        if (e == hipSuccess) e = hipMemcpy(S.span_tab, host_span, sizeof host_span, hipMemcpyHostToDevice);
         // CSR / verify calls take their scratch from the stream-ordered pool
         // (hipMallocAsync / hipFreeAsync on the caller's stream).  Keep freed
         // blocks in the pool across synchronisations: with the default
@@ -173,7 +179,10 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
 //   pairs    crc32c_pair.hip: 13 % fewer bytes, streamed at ~5.0 TB/s: 0.233 ms
 // The initial value comes from the environment (LNL_CSR_PATH=bucketed |
 // uniform | seg | pairs).
-enum CsrPath : int { kPathBucketed = 0, kPathUniform = 1, kPathSeg = 2, kPathPairs = 3 };
+// kPathBucketed (0) is the product: the span kernel for CSR batches, the
+// bucketed batch kernel for verify / filter batches; kPathBucketCsr (4) runs
+// CSR batches through the bucketed batch kernel too (the previous default)
+enum CsrPath : int { kPathBucketed = 0, kPathUniform = 1, kPathSeg = 2, kPathPairs = 3, kPathBucketCsr = 4 };
 #if !LNL_EXPERIMENTS
 constexpr int csr_path() { return kPathBucketed; }
 #else
@@ -186,6 +195,7 @@ int csr_path() {
         if (!strcmp(e, "uniform")) p = kPathUniform;
         else if (!strcmp(e, "seg")) p = kPathSeg;
         else if (!strcmp(e, "pairs")) p = kPathPairs;
+        else if (!strcmp(e, "bucketed")) p = kPathBucketCsr;
     }
     int expect = -1;
     g_csr_path.compare_exchange_strong(expect, p);
@@ -308,8 +318,44 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 }
 #endif  // LNL_EXPERIMENTS
 
+// CSR batches (product path): the span kernel (crc32c_span.hip: every line read
+// once, one 512-thread workgroup per CU) after its pre-pass, then the batch
+// kernel, which completes the cross-segment heads and takes the datagrams the
+// span kernel leaves (three or more segments; device-side count).
+int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
+    lnl::SpanArgs g{};
+    g.base = a.base;
+    g.off = a.off;
+    g.off0 = a.off0;
+    g.n = a.n;
+    g.waves = (uint32_t)S.cus * (uint32_t)(lnl::kSpanThreads / 64);
+    g.out = a.out;
+    g.tab = S.span_tab;
+    void* scratch = nullptr;
+    const size_t bytes = lnl::span_scratch_words(a.n, g.waves) * sizeof(uint32_t);
+    hipError_t e = hipMallocAsync(&scratch, bytes, st);
+    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
+    lnl::span_scratch_layout(g, (uint32_t*)scratch);
+    int rc = 0;
+    e = lnl::launch_span(g, S.cus, st);
+    if (e != hipSuccess) rc = hip_fail(e, "span kernel launch");
+    if (rc == 0) {
+        lnl::BatchArgs o = a;
+        o.perm = g.ovf;
+        o.perm_n = g.ctl + 1;
+        o.span_rec = g.rec;
+        o.span_ctl = g.ctl;
+        o.span_tab = S.span_tab;
+        rc = launch(S, o, lnl::kModeCsr, st);
+    }
+    e = hipFreeAsync(scratch, st);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
+}
+
 int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
     if (a.n < LNL_BUCKET_MIN_N) return launch(S, a, mode, st);
+    if (mode == lnl::kModeCsr && csr_path() == kPathBucketed) return launch_csr_span(S, a, st);
 #if LNL_EXPERIMENTS
     if (mode == lnl::kModeCsr) {
         switch (csr_path()) {
@@ -386,7 +432,7 @@ extern "C" int lnl_crc32c_abi_version(void) { return LNL_CRC32C_ABI_VERSION; }
 // kernel, 1 uniform, 2 segment, 3 pair; see csr_path above).  Returns the
 // previous path, or -EINVAL.
 extern "C" int lnl_crc32c_set_csr_path(int path) {
-    if (path < kPathBucketed || path > kPathPairs) return fail(-EINVAL, "CSR path %d out of range", path);
+    if (path < kPathBucketed || path > kPathBucketCsr) return fail(-EINVAL, "CSR path %d out of range", path);
     const int prev = csr_path();
     g_csr_path.store(path);
     return prev;
@@ -471,7 +517,8 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
     a.filter = filter;
     hipStream_t st = (hipStream_t)hip_stream;
     const int path = csr_path();
-    if (n < LNL_BUCKET_MIN_N || path == kPathBucketed) return launch_csr(*S, a, lnl::kModeVerify, st);
+    if (n < LNL_BUCKET_MIN_N || path == kPathBucketed || path == kPathBucketCsr)
+        return launch_csr(*S, a, lnl::kModeVerify, st);
 #if !LNL_EXPERIMENTS
     return fail(-EINVAL, "unreachable CSR path %d", path);
 #else

@@ -29,6 +29,11 @@ struct BatchArgs {
     const uint32_t* perm_n;  // optional (device): number of perm entries, else n
     const uint32_t* tail_xor;  // optional: out[i] ^= tail_xor[i] for all i < n first (CSR uniform path)
     uint32_t xor_n;            // entries of tail_xor
+    // optional (CSR span path): the span kernel's per-segment head / tail
+    // records, completed first (crc32c_span.h); span_ctl[2] = segments
+    const uint4* span_rec;
+    const uint32_t* span_ctl;
+    const uint32_t* span_tab;  // kSpanTabWords words (lnl_build_span_tables)
 };
 
 // Enqueue one batch kernel on `stream` with `grid` workgroups.
@@ -152,6 +157,29 @@ hipError_t launch_seg(const SegArgs& a, int grid, hipStream_t stream);
 // scratch words (u32) launch_seg needs for n datagrams on `waves` resident waves
 size_t seg_scratch_words(uint32_t n, uint32_t waves);
 void seg_scratch_layout(SegArgs& a, uint32_t* scratch);
+
+// CSR span path (crc32c_span.hip): every line of the stream read once, lane
+// g owns segment g; datagram folds batched wave-uniformly through an LDS
+// stash.  launch_span enqueues the counter reset, the pre-pass and the kernel;
+// the caller then runs the batch kernel over ovf (perm_n = ctl + 1) with
+// span_rec / span_ctl set, which completes the cross-segment heads first.
+constexpr int kSpanThreads = 512;  // one workgroup (8 waves) per CU
+struct SpanArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    uint64_t off0;
+    uint32_t n;
+    uint32_t waves;          // resident waves of the kernel's grid (CUs x 8)
+    uint32_t* out;
+    const uint32_t* tab;     // kSpanTabWords words (lnl_build_span_tables)
+    uint32_t* ctl;           // 4 words: [1] overflow datagrams, [2] segments
+    uint32_t* first;         // span_max_segments(waves) + 1
+    uint32_t* ovf;           // n: datagrams left to the batch kernel
+    uint4* rec;              // span_max_segments(waves) head / tail records
+};
+size_t span_scratch_words(uint32_t n, uint32_t waves);
+void span_scratch_layout(SpanArgs& a, uint32_t* scratch);
+hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream);
 
 // CSR uniform path (crc32c_csr.hip): plan pre-pass + uniform line-count
 // batches that fetch each shared boundary line once.  The caller then runs

@@ -48,6 +48,7 @@
 #include "crc32c_device.h"
 #include "crc32c_kernels.h"
 #include "lnl_packet.h"
+#include "crc32c_span.h"
 
 // Build knobs (defaults are the shipped configuration):
 //   LNL_GLDS_AUX   cache-policy bits of the LDS-DMA loads (0 = default, 2 = nt)
@@ -268,6 +269,19 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
         for (uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x; i < a.xor_n; i += gridDim.x * kBlockThreads) {
             const uint32_t v = a.tail_xor[i];
             if (v) a.out[i] ^= v;
+        }
+    }
+    // CSR span path: complete the datagrams that entered a segment from the
+    // previous one (crc32c_span.hip leaves both parts as register values per
+    // segment): CRC = ~step^(-8e)(step^(1024 m) tail ^ head), tables read from
+    // global memory
+    if (a.span_rec) {
+        const uint32_t ns = a.span_ctl[2];
+        for (uint32_t g = 1u + blockIdx.x * kBlockThreads + threadIdx.x; g < ns; g += gridDim.x * kBlockThreads) {
+            const uint4 h = a.span_rec[g];
+            if (!(h.z & kSpanHeadBit) || h.y >= a.n) continue;
+            const uint32_t m = h.z & 0xFFu, e = (h.z >> 8) & 0xFFu;
+            a.out[h.y] = lnl_span_final(a.span_tab, e, lnl_span_rows(a.span_tab, m, a.span_rec[g - 1u].w) ^ h.x);
         }
     }
     // entries to process: n, or a device-side count of perm entries

@@ -1,0 +1,630 @@
+// crc32c_span.hip -- CSR batches as line SEGMENTS with a wave-uniform fold
+// stash (config 3: 2^20 mixed-length datagrams; any CSR batch of >= 16 Ki
+// datagrams).
+//
+// A CSR batch is one contiguous byte stream (datagram i = base[off[i],
+// off[i+1])), so the shape that reads every 128-byte line exactly once with
+// every lane busy is the SEGMENT: lane l of wave-batch w owns segment
+// g = 64 w + l, R consecutive lines (crc32c_span.h), and reads line g R + t at
+// row t.  Measured on the probe (hbm_probe.hip, forms 4 and 7), that shape
+// streams at 6.8-6.9 TB/s.  What made the earlier segment kernel VALU-bound
+// was the FOLD: datagram ends fall on different rows in every lane, so nearly
+// every row paid a divergent 5-level fold (~720 VALU ops) for the few lanes
+// that ended a datagram.  Here a lane never folds its own datagram:
+//
+//  * Row step.  o = A s ^ x for every lane (one generated network,
+//    crc32c_bitslice.h).  A lane whose datagram ends in this row at byte b-1
+//    has state o ^ F(b), where F(b) is the row from byte b on (pieces before
+//    b's piece read from a zero piece, b's piece AND-masked in place in LDS);
+//    the next datagram starts with state F(b) ^ C[b] (CRC init as word 0).
+//    Further datagrams that start and end inside the row: F(b) ^ F(b') ^ C[b].
+//    The row's network runs once whatever the boundaries are.
+//  * Stash.  Ended states (32 words) go to a per-wave LDS ring (kCap entries)
+//    with their datagram index and e (bytes of the row after the last one).
+//    When 64 are waiting, the whole wave folds 64 of them at once -- one per
+//    lane, uniform: a table Horner straight to the CRC register (crc32c_span.h,
+//    ~200 VALU ops and 128 byte-table lookups), then the final map (two
+//    nibble-table products) -- and stores the CRCs.  Fold cost per datagram:
+//    one fold, never a divergent one.
+//  * Heads and tails.  A datagram that runs in from the previous segment (the
+//    head) is folded from state 0; the previous lane folds the part it saw
+//    (the tail).  CRC registers are linear:
+//    CRC = ~step^(-8e)(step^(1024 m) tail ^ head).  The
+//    kernel leaves both per segment (crc32c_span.h record), and the batch
+//    kernel's prologue (crc32c_kernels.hip) combines them before it takes the
+//    datagrams touching three or more segments (the overflow list).
+//
+// Memory: rows come in as 16-byte pieces, glds-shaped (load i of lane l is
+// piece l & 7 of the row of lane 8 i + l / 8: 8 whole lines per
+// wave-instruction), into VGPRs -- two rows in flight -- and are transposed
+// through an 8 KiB LDS image per wave (the probe's form 7).  That leaves LDS
+// for the stash: 17 KiB of fold tables + 8 waves x (8 KiB image + 66 x 152 B
+// stash and meta) = 163,328 B, one 512-thread workgroup per CU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_device.h"
+#include "crc32c_kernels.h"
+#include "crc32c_span.h"
+
+namespace lnl {
+
+namespace {
+
+using namespace dev;
+
+constexpr int kThreads = kSpanThreads;
+constexpr int kWaves = kThreads / 64;
+constexpr uint32_t kCap = 66;      // stash entries per wave
+constexpr uint32_t kFlush = 64;    // fold when this many are waiting
+constexpr uint32_t kEntry = 144;   // stash entry stride: 128 B of state + 16 B pad, so that
+                                   // consecutive slots start on different banks and the 8
+                                   // pieces of an entry sit at immediate offsets
+constexpr uint32_t kImageBytes = 8192;
+constexpr uint32_t kTabBytes = kSpanTabLds * 4;
+// LDS (bytes): the fold tables (crc32c_span.h) first -- the Horner's byte
+// lookups then address them with a 16-bit immediate offset -- and a zero
+// piece; the waves' row images (8 KiB each, 128-byte aligned, so piece p of a
+// swizzled row is r0 ^ 16 p); the stashes and their meta words
+constexpr uint32_t kTabOff = 0;
+constexpr uint32_t kZeroOff = kTabOff + kTabBytes;
+constexpr uint32_t kImageOff = (kZeroOff + 16u + 127u) & ~127u;
+constexpr uint32_t kStashOff = kImageOff + kWaves * kImageBytes;
+constexpr uint32_t kStashBytes = kCap * kEntry;
+constexpr uint32_t kMetaOff = kStashOff + kWaves * kStashBytes;
+constexpr uint32_t kLdsBytes = kMetaOff + kWaves * kCap * 8;
+static_assert(kLdsBytes <= 160 * 1024, "LDS");
+static_assert(kTabBytes % 16 == 0 && kStashOff % 16 == 0 && kMetaOff % 8 == 0, "LDS alignment");
+
+enum : uint32_t { kTypeNormal = 0, kTypeHead = 1, kTypeTail = 2 };
+
+__device__ LNL_INLINE SpanGeo geometry_of(const SpanArgs& a) {
+    const uint64_t b = (uint64_t)(uintptr_t)a.base - a.off0;
+    return span_geometry(b + a.off[0], b + a.off[a.n], a.waves);
+}
+
+// ceil(P / (128 R)) for a byte offset P from S0
+__device__ LNL_INLINE uint32_t seg_ceil(uint64_t P, uint32_t R) {
+    const uint64_t lines = (P + 127u) >> 7;
+    return (uint32_t)((lines + R - 1u) / R);
+}
+
+// ---- pre-pass ---------------------------------------------------------------
+
+__device__ LNL_INLINE void append(uint32_t* cnt, uint32_t* list, bool take, uint32_t value) {
+    const uint64_t m = __ballot(take);
+    if (m == 0ull) return;
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)leader, 64);
+    if (take) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = value;
+}
+
+// One thread per datagram: first[g] = min{ i : P_{i+1} > g Sb } for the g in
+// [ceil(P_i / Sb), ceil(P_{i+1} / Sb)) (first[NS] = n); CRC 0 for empty
+// datagrams; the overflow list; ctl[2] = segments.  A batch the kernel does not
+// take goes to the batch kernel whole.
+__global__ __launch_bounds__(256) void span_prep_kernel(SpanArgs a) {
+    const uint64_t b = (uint64_t)(uintptr_t)a.base - a.off0;
+    const SpanGeo G = geometry_of(a);
+    const bool whole = !span_runs(G, a.waves);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ctl[2] = whole ? 0u : G.NS;
+        if (whole) a.ctl[1] = a.n;
+    }
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+        if (whole) {
+            a.ovf[i] = i;
+            continue;
+        }
+        const uint64_t Pi = b + a.off[i] - G.S0, Pj = b + a.off[i + 1] - G.S0;
+        if (Pi == Pj) a.out[i] = 0u;  // CRC-32C of zero bytes
+        append(&a.ctl[1], a.ovf, Pj > Pi && span_overflow(Pi, Pj, G.R), i);
+        const uint32_t lo = i == 0 ? 0u : seg_ceil(Pi, G.R), hi = seg_ceil(Pj, G.R);
+        for (uint32_t g = lo; g < hi; ++g) a.first[g] = i;
+        if (i + 1u == a.n) a.first[G.NS] = a.n;
+    }
+}
+
+// ---- the span kernel ---------------------------------------------------------
+
+// The lane's upcoming datagram boundaries (byte offsets from its segment's
+// first byte, clamped to 0xFFFF), two 16-bit entries per register, the front
+// in q[0]'s low half.
+struct Queue {
+    uint32_t q[8];
+    __device__ LNL_INLINE uint32_t front() const { return q[0] & 0xFFFFu; }
+    __device__ LNL_INLINE void pop() {
+#pragma unroll
+        for (int j = 0; j < 7; ++j) q[j] = __builtin_amdgcn_alignbit(q[j + 1], q[j], 16);
+        q[7] = (q[7] >> 16) | 0xFFFF0000u;
+    }
+};
+
+__device__ constexpr uint32_t kZero32[32] = {0u};
+
+__device__ LNL_INLINE uint32_t clamp16(int64_t v) { return v <= 0 ? 0u : (v >= 0xFFFF ? 0xFFFFu : (uint32_t)v); }
+
+// ~step^(-8e)(r): the final map (two nibble-table products, LDS)
+__device__ LNL_INLINE uint32_t final_crc_lds(uint32_t tab_base, uint32_t e, uint32_t r) {
+    r = fold_apply_lds(tab_base + 4u * kSpanTabB + 512u * (e & 15u), r);
+    r = fold_apply_lds(tab_base + 4u * kSpanTabA + 512u * (e >> 4), r);
+    return ~r;
+}
+
+// The register value of a 32-word state: lnl_span_phi (crc32c_span.h) with
+// the byte tables in LDS -- four independent Horner chains, joined by step^256
+__device__ LNL_INLINE uint32_t phi_lds(const uint32_t* T, uint32_t tab_base, const uint32_t* v) {
+    uint32_t r0 = 0u, r1 = 0u, r2 = 0u, r3 = 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        r0 = lnl_span_t4(T, r0 ^ v[k]);
+        r1 = lnl_span_t4(T, r1 ^ v[8 + k]);
+        r2 = lnl_span_t4(T, r2 ^ v[16 + k]);
+        r3 = lnl_span_t4(T, r3 ^ v[24 + k]);
+    }
+    const uint32_t s = tab_base + 4u * kSpanTabS;
+    r1 ^= fold_apply_lds(s, r0);
+    r2 ^= fold_apply_lds(s, r1);
+    return r3 ^ fold_apply_lds(s, r2);
+}
+
+// 16 bytes of a row from global memory, nt, in inline asm: the compiler does
+// not see these loads, so it inserts no waits for them; row_step waits with a
+// counted vmcnt(8) (a row step issues the 8 loads of row t + 2; at row t the
+// other buffer's 8 loads of row t + 1 are the younger ones).  Left to the compiler, its vmcnt for one buffer
+// counted the other buffer's loads as older and drained both every step.
+__device__ LNL_INLINE void row_load(u32x4& v, uint64_t addr) {
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(addr) : "memory");
+}
+
+// 16 bytes to LDS at addr + OFF (immediate offset)
+template <uint32_t OFF>
+__device__ LNL_INLINE void ds_write16(uint32_t addr, u32x4 v) {
+    asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
+}
+
+// 8 x 16 bytes from LDS at base + 16 p (immediate offsets) + lgkmcnt(0)
+__device__ LNL_INLINE void ds_read8(uint32_t base, uint32_t* x) {
+    uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+    asm volatile(
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %1, %8 offset:16\n\t"
+        "ds_read_b128 %2, %8 offset:32\n\t"
+        "ds_read_b128 %3, %8 offset:48\n\t"
+        "ds_read_b128 %4, %8 offset:64\n\t"
+        "ds_read_b128 %5, %8 offset:80\n\t"
+        "ds_read_b128 %6, %8 offset:96\n\t"
+        "ds_read_b128 %7, %8 offset:112\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(v4), "=&v"(v5), "=&v"(v6), "=&v"(v7)
+        : "v"(base)
+        : "memory");
+    const uint4 v[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        x[4 * k + 0] = v[k].x;
+        x[4 * k + 1] = v[k].y;
+        x[4 * k + 2] = v[k].z;
+        x[4 * k + 3] = v[k].w;
+    }
+}
+
+template <int P>
+struct Pieces {  // the 8 pieces of a 32-word state written at base + 16 p
+    __device__ static LNL_INLINE void write(uint32_t base, const uint32_t* x, const uint32_t* y) {
+        u32x4 w;
+        w.x = x[4 * P + 0] ^ y[4 * P + 0];
+        w.y = x[4 * P + 1] ^ y[4 * P + 1];
+        w.z = x[4 * P + 2] ^ y[4 * P + 2];
+        w.w = x[4 * P + 3] ^ y[4 * P + 3];
+        ds_write16<16 * P>(base, w);
+        Pieces<P + 1>::write(base, x, y);
+    }
+};
+template <>
+struct Pieces<8> {
+    __device__ static LNL_INLINE void write(uint32_t, const uint32_t*, const uint32_t*) {}
+};
+
+template <int I>
+struct Transpose {  // load i of the row to the image: even i at we + 1024 i, odd at wo + 1024 i
+    __device__ static LNL_INLINE void write(uint32_t we, uint32_t wo, const u32x4* cur) {
+        ds_write16<1024 * I>((I & 1) ? wo : we, cur[I]);
+        Transpose<I + 1>::write(we, wo, cur);
+    }
+};
+template <>
+struct Transpose<8> {
+    __device__ static LNL_INLINE void write(uint32_t, uint32_t, const u32x4*) {}
+};
+
+__global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
+    __shared__ __attribute__((aligned(128))) uint8_t lds[kLdsBytes];
+    const uint32_t lane = __lane_id();
+    const uint32_t wave = uni(threadIdx.x >> 6);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+    const uint32_t tab_base = lds0 + kTabOff;
+    const uint32_t* const T = reinterpret_cast<const uint32_t*>(lds + kTabOff) + kSpanTabT;
+    const uint32_t zero_addr = lds0 + kZeroOff;
+    const uint32_t image = lds0 + kImageOff + wave * kImageBytes;
+    const uint32_t stash = lds0 + kStashOff + wave * kStashBytes;
+    const uint32_t meta = lds0 + kMetaOff + wave * (kCap * 8u);
+    const uint32_t* const ctab = reinterpret_cast<const uint32_t*>(lds + kTabOff) + kSpanTabC;  // C[pad]
+
+    const uint64_t bsh = (uint64_t)(uintptr_t)A.base - A.off0;
+    const SpanGeo G = geometry_of(A);
+    if (!span_runs(G, A.waves)) return;
+    const uint32_t R = G.R, Sb = R << 7, NS = G.NS, nwb = G.nwb;
+    if (blockIdx.x * kWaves >= nwb) return;  // whole workgroup idle (before the barrier)
+    {
+        const uint4* f = reinterpret_cast<const uint4*>(A.tab);
+        uint4* fl = reinterpret_cast<uint4*>(lds + kTabOff);
+        for (uint32_t i = threadIdx.x; i < kTabBytes / 16u; i += kThreads) fl[i] = f[i];
+        if (threadIdx.x == 0) *reinterpret_cast<uint4*>(lds + kZeroOff) = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+    }
+    const uint32_t gw = blockIdx.x * kWaves + wave;
+    const uint32_t nw = gridDim.x * kWaves;
+    const uint32_t n = A.n;
+
+    // per-lane addressing: load i brings piece pc of the row of lane 8 i + sub;
+    // it lands in the image at that lane's row, slot pc ^ swz(8 i + sub)
+    // (= pc ^ (sub >> 1) for even i, ^ 4 more for odd i)
+    const uint32_t sub = lane >> 3, pc = lane & 7u;
+    const uint32_t voff = sub * Sb + 16u * pc;
+    const uint32_t we = image + sub * 128u + 16u * (pc ^ (sub >> 1));
+    const uint32_t wo = we ^ 64u;
+    const uint32_t r0 = image + lane * 128u + 16u * swz(lane);  // piece p of this lane's row: r0 ^ 16 p
+    const uint64_t last_line = (G.S0 + G.Pn - 1u) & ~(uint64_t)127;
+
+    for (uint32_t wb = gw; wb < nwb; wb += nw) {
+        const uint64_t line0 = G.S0 + (uint64_t)wb * 64u * Sb;
+        const bool clamp = line0 + 64ull * Sb - 128u > last_line;
+        // row t of the wave-batch: load i of this lane is piece pc of line
+        // line0 + (8 i + sub) Sb + 128 t (clamped to the stream's last line in
+        // the last wave-batches)
+        const uint32_t last_rel = (uint32_t)(last_line - line0 < 0xFFFFFFFFull ? last_line - line0 : 0xFFFFFFFFull);
+        auto issue = [&](uint32_t t, u32x4* v) {
+            if (!clamp) {
+                const uint64_t rbase = line0 + ((uint64_t)t << 7);
+                uint32_t vo = voff;
+                asm volatile("" : "+v"(vo));  // 8 per-load addresses per row, not hoisted into 16 registers
+#pragma unroll
+                for (int i = 0; i < 8; ++i) row_load(v[i], rbase + (uint64_t)(i * 8u * Sb) + vo);
+            } else {
+                uint32_t lo = (sub * Sb) + (t << 7);
+                asm volatile("" : "+v"(lo));
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    uint32_t rel = lo + (uint32_t)i * 8u * Sb;
+                    rel = rel > last_rel ? last_rel : rel;
+                    row_load(v[i], line0 + rel + 16u * pc);
+                }
+            }
+        };
+        u32x4 ra[8], rb[8];
+        issue(0u, ra);
+        issue(1u, rb);  // R >= 16
+
+        // ---- this lane's datagrams ----------------------------------------
+        const uint32_t g = wb * 64u + lane;
+        const bool live = g < NS;
+        const uint64_t segbase = line0 + (uint64_t)lane * Sb;
+        const uint32_t k0 = live ? A.first[g] : n;
+        const uint32_t k1 = live ? A.first[g + 1u] : n;  // [k0, k1): datagrams ending in this segment
+        Queue Q;
+        uint32_t k = k0, kq, qn;
+        int32_t cs;  // first byte of datagram k, from the segment's first byte
+        uint32_t inj = 0u;
+        {
+            const int64_t d0 = k0 < n ? (int64_t)(bsh + A.off[k0]) - (int64_t)segbase : 0;
+            cs = d0 < -(int64_t)(2u * Sb + 2u) ? -(int32_t)(2u * Sb + 2u) : (int32_t)d0;
+            // 16 boundaries, loaded together (indices clamped, values selected;
+            // the empty asm keeps the compiler from sinking each load into its
+            // own branch, which would wait for them one by one)
+            uint64_t ov[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t kk = k0 + (uint32_t)j + 1u;
+                ov[j] = A.off[kk < n ? kk : n];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(ov[j]));
+            uint32_t qp[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t lo = clamp16((int64_t)(bsh + ov[2 * j]) - (int64_t)segbase);
+                const uint32_t hi = clamp16((int64_t)(bsh + ov[2 * j + 1]) - (int64_t)segbase);
+                const uint32_t vlo = k0 + 2u * j < n ? lo : 0xFFFFu, vhi = k0 + 2u * j + 1u < n ? hi : 0xFFFFu;
+                qp[j] = vlo | (vhi << 16);
+            }
+            // segment 0: the bytes before the batch's first datagram end a
+            // virtual, untracked datagram k0 - 1 at boundary cs (queue shifted
+            // by one entry)
+            const bool virt = k0 < n && cs > 0;
+            Q.q[0] = virt ? ((uint32_t)cs | (qp[0] << 16)) : qp[0];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) Q.q[j] = virt ? __builtin_amdgcn_alignbit(qp[j], qp[j - 1], 16) : qp[j];
+            kq = virt ? k0 + 15u : k0 + 16u;
+            qn = 16u;
+            if (virt) {
+                k = k0 - 1u;
+                cs = -(int32_t)(2u * Sb + 2u);
+            } else if (k0 < n && cs == 0) {
+                inj = 0xFFFFFFFFu;  // C[0]: datagram k0 starts at row 0, byte 0
+            }
+        }
+        // k0 < n: the lane has a datagram open (k0 - 1 when virtual)
+        const bool open0 = k0 < n;
+        auto is_open = [&]() { return open0 && (k < n || k == k0 - 1u); };
+        auto refill = [&]() {
+            // lanes whose queue is empty while a datagram is still open: the
+            // next 16 boundaries (rare: > 16 datagrams in one segment)
+            const bool need = qn == 0u && is_open() && k <= k1;
+            if (__any(need)) {
+                if (need) {
+                    uint64_t ov[16];
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const uint32_t kk = kq + (uint32_t)j + 1u;
+                        ov[j] = A.off[kk < n ? kk : n];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(ov[j]));
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t ka = kq + 2u * j, kb = ka + 1u;
+                        const uint32_t lo = clamp16((int64_t)(bsh + ov[2 * j]) - (int64_t)segbase);
+                        const uint32_t hi = clamp16((int64_t)(bsh + ov[2 * j + 1]) - (int64_t)segbase);
+                        Q.q[j] = (ka < n ? lo : 0xFFFFu) | ((kb < n ? hi : 0xFFFFu) << 16);
+                    }
+                    kq += 16u;
+                    qn = 16u;
+                }
+            }
+        };
+
+        // ---- stash (wave-uniform counters) ---------------------------------
+        uint32_t st_head = 0, st_tail = 0, head_slot = 0, tail_slot = 0;
+        uint32_t hpos = 0, tpos = 0, r_head = 0, r_tail = 0, hk = 0, hinfo = 0;
+        bool hpend = false, tpend = false, htrack = false, ttrack = false;
+
+        // Fold the nf oldest entries, one per lane.  The caller's live state
+        // (32 words) waits in the stash meanwhile -- lane l < nf in the slot
+        // it has just read, the others in free slots (cnt + 64 - nf <= kCap)
+        // -- so the fold's registers do not come on top of it.
+        auto flush = [&](uint32_t nf, uint32_t* live_state) {
+            const bool act = lane < nf;
+            uint32_t slot = act ? head_slot + lane : tail_slot + (lane - nf);
+            slot = slot >= kCap ? slot - kCap : slot;
+            const uint32_t ea = stash + slot * kEntry;
+            uint32_t v[32];
+            ds_read8(ea, v);
+            uint2 mt;
+            asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(mt) : "v"(meta + slot * 8u) : "memory");
+            Pieces<0>::write(ea, live_state, kZero32);
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 1)
+            const uint32_t r = v[0] ^ v[31];  // diagnostic build only: no fold (wrong CRCs)
+#else
+            const uint32_t r = phi_lds(T, tab_base, v);
+#endif
+            const uint32_t type = (mt.y >> 8) & 3u, e = mt.y & 127u;
+            const uint32_t crc = final_crc_lds(tab_base, e, r);
+            if (act && type == kTypeNormal && mt.x < n) A.out[mt.x] = crc;  // (the index check only guards the store)
+            // head / tail folds back to the lanes that own them
+            const uint32_t hs = hpos - st_head, ts = tpos - st_head;
+            const uint32_t rh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (hs & 63u)), (int)r);
+            const uint32_t rt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (ts & 63u)), (int)r);
+            if (hpend && hs < nf) {
+                r_head = rh;
+                hpend = false;
+            }
+            if (tpend && ts < nf) {
+                r_tail = rt;
+                tpend = false;
+            }
+            ds_read8(ea, live_state);
+            st_head += nf;
+            head_slot += nf;
+            head_slot = head_slot >= kCap ? head_slot - kCap : head_slot;
+        };
+        // append P ^ F (32 words, registers) for the lanes that take
+        auto put = [&](bool take, const uint32_t* P, const uint32_t* F, uint32_t info) -> uint32_t {
+            const uint64_t m = __ballot(take);
+            const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            uint32_t slot = tail_slot + rank;
+            slot = slot >= kCap ? slot - kCap : slot;
+            if (take) {
+                Pieces<0>::write(stash + slot * kEntry, P, F);
+                const uint2 mt = make_uint2(k, info);
+                asm volatile("ds_write_b64 %0, %1" ::"v"(meta + slot * 8u), "v"(mt) : "memory");
+            }
+            const uint32_t pos = st_tail + rank;
+            const uint32_t c = (uint32_t)__popcll(m);
+            st_tail += c;
+            tail_slot += c;
+            tail_slot = tail_slot >= kCap ? tail_slot - kCap : tail_slot;
+            return pos;
+        };
+
+        // One boundary per lane that has one (ev): the datagram open in
+        // sout ends at row byte b - 1 -- its state sout ^ F(b) goes to the
+        // stash when it is tracked (take) -- and the next one starts at b
+        // with state F(b) ^ C[b].  F(b) = the row from byte b on: b's piece
+        // AND-masked in place in the image, earlier pieces from a zero piece.
+        auto boundary = [&](uint32_t t, bool ev, bool zero, uint32_t b, bool take, uint32_t* sout) {
+            {
+                const uint32_t nst = (uint32_t)__popcll(__ballot(take));
+                const uint32_t cnt = st_tail - st_head;
+                if (nst && (cnt >= kFlush || cnt + nst > kCap)) flush(cnt < kFlush ? cnt : kFlush, sout);
+            }
+            const bool start = ev && !zero;
+            const uint32_t c0 = ctab[b & 127u];
+            if (start && b < 128u) {
+                // keep the piece's bytes >= d: bits >= 8 d of the 128-bit piece
+                const uint32_t d = b & 15u;
+                const uint64_t lo = d < 8u ? ~0ull << (8u * d) : 0ull;
+                const uint64_t hi = d < 8u ? ~0ull : ~0ull << (8u * (d - 8u));
+                const uint32_t m[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+                patch_piece<0>(r0 ^ (16u * (b >> 4)), m);
+            }
+            uint32_t F[32];
+            {
+                const uint32_t bp = start ? (b >> 4) : 8u;
+                uint32_t ad[8];
+#pragma unroll
+                for (int p = 0; p < 8; ++p) ad[p] = (uint32_t)p < bp ? zero_addr : r0 ^ (16u * p);
+                read_row<0>(ad, F);
+            }
+            const bool head = cs < 0;
+            const uint32_t pos = put(take, sout, F, (128u - b) | ((head ? kTypeHead : kTypeNormal) << 8));
+            if (take && head) {
+                hpos = pos;
+                hpend = true;
+                htrack = true;
+                hk = k;
+                hinfo = (t + 1u) | ((128u - b) << 8);
+            }
+            if (ev) {
+                Q.pop();
+                --qn;
+                ++k;
+            }
+            if (start) {
+                cs = (int32_t)((t << 7) + b);
+                inj = b == 128u ? 0xFFFFFFFFu : 0u;  // C[0] at the next row's word 0
+            }
+#pragma unroll
+            for (int w = 0; w < 32; ++w) sout[w] = start ? F[w] : sout[w];
+            sout[0] ^= start && b < 128u ? c0 : 0u;
+        };
+
+        // ---- rows ---------------------------------------------------------
+        // Row step: sout = A sin ^ row, then every datagram boundary in the
+        // row (usually at most one per lane): the ended datagram's state
+        // sout ^ F(b) goes to the stash, and sout = F(b) ^ C[b] starts the
+        // next one.  sin / sout alternate between two arrays (no copies).
+        auto row_step = [&](uint32_t t, u32x4* cur, uint32_t* sin, uint32_t* sout) {
+            // the row into the image (8 lanes' lines per load), then this
+            // buffer takes row t + 2.  The other buffer's 8 loads (row t + 1)
+            // are younger; the last row waits for everything, so no row load
+            // is in flight once the loop ends (the compiler does not see them
+            // and would hand their registers to the epilogue)
+            if (t + 1u < R)
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            Transpose<0>::write(we, wo, cur);
+            if (t + 2u < R) issue(t + 2u, cur);
+            {
+                uint32_t x[32], rad[8], rr = r0;
+                asm volatile("" : "+v"(rr));  // 7 XORs per row rather than 8 registers held
+#pragma unroll
+                for (int p = 0; p < 8; ++p) rad[p] = rr ^ (16u * p);
+                read_row<0>(rad, x);
+                lnl_net_row_x(sin, x, sout);
+            }
+            sout[0] ^= inj;
+            inj = 0u;
+            const uint32_t rowst = t << 7, rowend = rowst + 128u;
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 2)
+            return;  // diagnostic build only: rows and networks, no datagram boundaries
+#endif
+            bool ev = is_open() && Q.front() <= rowend;
+            if (!__any(ev)) return;
+            // the first boundary of every lane (straight-line; rows with two or
+            // more boundaries in one lane loop below)
+            {
+                const uint32_t b = ev ? Q.front() - rowst : 128u;
+                const bool take = ev && cs >= -(int32_t)Sb;  // (a row's first boundary never ends an empty datagram)
+                boundary(t, ev, false, b, take, sout);
+            }
+            refill();
+            ev = is_open() && Q.front() <= rowend;
+            while (__any(ev)) {
+                const uint32_t b = ev ? Q.front() - rowst : 128u;
+                const bool zero = ev && cs == (int32_t)(rowst + b);  // empty datagram (CRC written by the pre-pass)
+                const bool take = ev && !zero;                     // (started in this row: never a head)
+                boundary(t, ev, zero, b, take, sout);
+                refill();
+                ev = is_open() && Q.front() <= rowend;
+            }
+        };
+
+        uint32_t sA[32], sB[32];
+#pragma unroll
+        for (int w = 0; w < 32; ++w) sA[w] = 0u;
+        for (uint32_t t = 0; t < R; t += 2u) {
+            row_step(t, ra, sA, sB);
+            if (t + 1u < R)
+                row_step(t + 1u, rb, sB, sA);
+            else {
+#pragma unroll
+                for (int w = 0; w < 32; ++w) sA[w] = sB[w];
+            }
+        }
+
+        // ---- the tail: the datagram still open, if it started here and ends
+        // in the next segment; then fold everything still waiting -----------
+        refill();
+        {
+            const bool tail = is_open() && k < n && cs >= 0 && cs < (int32_t)Sb && Q.front() <= 2u * Sb;
+            bool tdone = !tail;
+            for (;;) {
+                const uint32_t nst = (uint32_t)__popcll(__ballot(!tdone));
+                const uint32_t cnt = st_tail - st_head;
+                if (nst == 0u && cnt == 0u) break;
+                if (nst == 0u || cnt >= kFlush || cnt + nst > kCap) {
+                    flush(cnt < kFlush ? cnt : kFlush, sA);
+                    continue;
+                }
+                const uint32_t pos = put(!tdone, sA, kZero32, kTypeTail << 8);
+                if (!tdone) {
+                    tpos = pos;
+                    tpend = true;
+                    ttrack = true;
+                }
+                tdone = true;
+            }
+        }
+        if (live)
+            A.rec[g] = make_uint4(r_head, hk, hinfo | (htrack ? kSpanHeadBit : 0u) | (ttrack ? kSpanTailBit : 0u),
+                                  r_tail);
+    }
+}
+
+}  // namespace
+
+size_t span_scratch_words(uint32_t n, uint32_t waves) {
+    const size_t ns = span_max_segments(waves);
+    size_t w = 4 + (ns + 1) + n;
+    w = (w + 3) & ~(size_t)3;  // rec[] is 16-byte aligned
+    return w + 4 * ns;
+}
+
+void span_scratch_layout(SpanArgs& a, uint32_t* s) {
+    const size_t ns = span_max_segments(a.waves);
+    a.ctl = s;
+    a.first = s + 4;
+    a.ovf = a.first + ns + 1;
+    size_t w = 4 + (ns + 1) + a.n;
+    w = (w + 3) & ~(size_t)3;
+    a.rec = reinterpret_cast<uint4*>(s + w);
+}
+
+hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(a.ctl, 0, 4 * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const uint32_t blocks = (a.n + 255u) / 256u;
+    const uint32_t prep = blocks < 8192u ? blocks : 8192u;
+    hipLaunchKernelGGL(span_prep_kernel, dim3(prep), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(crc32c_span_kernel, dim3(grid), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace lnl

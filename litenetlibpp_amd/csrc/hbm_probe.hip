@@ -91,12 +91,13 @@ __global__ __launch_bounds__(256) void seg_read_vgpr(const uint8_t* __restrict__
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
-__global__ __launch_bounds__(256) void seg_read_lds(const uint8_t* __restrict__ p, uint32_t nseg,
-                                                    uint32_t* __restrict__ sink) {
-    __shared__ __attribute__((aligned(16))) uint4 lds[4 * 2 * 512];  // 2 x 8 KiB per wave
+template <int kW>
+__global__ __launch_bounds__(64 * kW) void seg_read_lds(const uint8_t* __restrict__ p, uint32_t nseg,
+                                                       uint32_t* __restrict__ sink) {
+    __shared__ __attribute__((aligned(16))) uint4 lds[kW * 2 * 512];  // 2 x 8 KiB per wave
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t gw = blockIdx.x * 4u + wave, nw = gridDim.x * 4u;
+    const uint32_t gw = blockIdx.x * kW + wave, nw = gridDim.x * kW;
     uint4* const buf = lds + wave * 1024;
     const uint32_t sub = lane >> 3, piece = lane & 7u;
     uint32_t acc = 0;
@@ -134,17 +135,71 @@ __global__ __launch_bounds__(256) void seg_read_lds(const uint8_t* __restrict__ 
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// form 7: the same pieces as form 4 (8 lines per wave-instruction), loaded
+// into VGPRs (global_load_dwordx4 nt), two rows in flight in registers, then
+// written to an 8 KiB LDS scratch (ds_write_b128 x 8) and read back as the
+// lane's own row: half the LDS of form 4 per wave
+__global__ __launch_bounds__(256) void seg_read_staged(const uint8_t* __restrict__ p, uint32_t nseg,
+                                                       uint32_t* __restrict__ sink) {
+    __shared__ __attribute__((aligned(16))) uint4 lds[4 * 512];  // 8 KiB per wave
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t gw = blockIdx.x * 4u + wave, nw = gridDim.x * 4u;
+    uint4* const buf = lds + wave * 512;
+    const uint32_t sub = lane >> 3, piece = lane & 7u;
+    uint32_t acc = 0;
+    for (uint32_t wb = gw; wb * 64u < nseg; wb += nw) {
+        const uint8_t* base = p + (size_t)wb * 64u * kSegR * 128u;
+        const uint32_t last = nseg - 1u - wb * 64u;
+        u32x4 a[8], b[8];
+        auto load = [&](uint32_t t, u32x4* v) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t q = 8u * i + sub;
+                const uint32_t qq = q < last ? q : last;
+                v[i] = __builtin_nontemporal_load((const u32x4*)(base + ((size_t)qq * kSegR + t) * 128u + 16u * piece));
+            }
+        };
+        auto consume = [&](const u32x4* v) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) buf[64 * i + lane] = *(const uint4*)&v[i];
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+            const uint4* r = buf + lane * 8;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc ^= r[k].x ^ r[k].y ^ r[k].z ^ r[k].w;
+        };
+        load(0, a);
+        load(1, b);
+        for (uint32_t t = 0; t < kSegR; t += 2) {
+            consume(a);
+            if (t + 2 < kSegR) load(t + 2, a);
+            consume(b);
+            if (t + 3 < kSegR) load(t + 3, b);
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 extern "C" int lnl_probe_stream_read(const void* d, size_t bytes, uint32_t* d_sink, void* stream, int form) {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int grid = cus * 2;
-    if (form >= 2 && form <= 4) {
+    if (form >= 2 && form <= 7) {
         const size_t nseg = bytes / (kSegR * 128u);
         if (nseg == 0 || nseg > 0xFFFFFFFFull) return -22;
         const uint32_t ns = (uint32_t)nseg;
         if (form == 4)
-            hipLaunchKernelGGL(seg_read_lds, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d, ns,
+            hipLaunchKernelGGL(seg_read_lds<4>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d, ns,
+                               d_sink);
+        else if (form == 5)  // one 5-wave workgroup per CU
+            hipLaunchKernelGGL(seg_read_lds<5>, dim3(cus), dim3(320), 0, (hipStream_t)stream, (const uint8_t*)d, ns,
+                               d_sink);
+        else if (form == 6)  // one 6-wave workgroup per CU
+            hipLaunchKernelGGL(seg_read_lds<6>, dim3(cus), dim3(384), 0, (hipStream_t)stream, (const uint8_t*)d, ns,
+                               d_sink);
+        else if (form == 7)
+            hipLaunchKernelGGL(seg_read_staged, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d, ns,
                                d_sink);
         else if (form == 3)
             hipLaunchKernelGGL(seg_read_vgpr<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream,

@@ -73,3 +73,19 @@ def test_segment_kernel_emulation(tmp_path):
     r = subprocess.run([str(exe), "0.2"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bad=0" in r.stdout
+
+
+def test_span_fold_tables(tmp_path):
+    """tests/emu/emu_span_fold.cpp: the span kernel's table-Horner fold and
+    register-basis final map equal the bit-sliced fold tree and the batch
+    kernels' final map for random states and every e; its row powers are
+    step^(1024 m); single-row datagrams match the oracle."""
+    oracle.load()
+    exe = tmp_path / "emu_span_fold"
+    src = os.path.join(ROOT, "tests", "emu", "emu_span_fold.cpp")
+    so_dir = os.path.dirname(oracle.ORACLE_SO)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src, f"-L{so_dir}",
+                    "-lcrc32c_oracle", f"-Wl,-rpath,{so_dir}"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bad=0" in r.stdout

@@ -21,6 +21,9 @@ VDIR = os.path.join(ROOT, "litenetlibpp_amd", "build", "variants")
 
 VARIANTS = {
     "base": "",                                     # shipped: lane-run kernel for fixed strides
+    "span_nofold": "-DLNL_SPAN_DIAG=1",             # CSR span kernel without its folds (wrong CRCs)
+    "span_noev": "-DLNL_SPAN_DIAG=2",               # CSR span kernel: rows + network only (wrong CRCs)
+    "bucketed": ("", 4),                            # CSR: the bucketed batch kernel (previous default)
     "batch": "-DLNL_NO_RUN",                        # any-layout batch kernel for everything
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
     "k16": "-DLNL_RUN_K=16",
