@@ -160,7 +160,7 @@ void seg_scratch_layout(SegArgs& a, uint32_t* scratch);
 
 // CSR span path (crc32c_span.hip): every line of the stream read once, lane
 // g owns segment g; datagram folds batched wave-uniformly through an LDS
-// stash.  launch_span enqueues the counter reset, the pre-pass and the kernel;
+// stash.  launch_span enqueues the pre-pass and the kernel;
 // the caller then runs the batch kernel over ovf (perm_n = ctl + 1) with
 // span_rec / span_ctl set, which completes the cross-segment heads first.
 constexpr int kSpanThreads = 512;  // one workgroup (8 waves) per CU

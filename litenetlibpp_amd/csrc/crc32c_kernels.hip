@@ -271,13 +271,15 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
             if (v) a.out[i] ^= v;
         }
     }
-    // CSR span path: complete the datagrams that entered a segment from the
-    // previous one (crc32c_span.hip leaves both parts as register values per
-    // segment): CRC = ~step^(-8e)(step^(1024 m) tail ^ head), tables read from
-    // global memory
+    // CSR span path: complete the datagrams that entered a wave-batch's first
+    // segment from the previous wave-batch's last one (crc32c_span.hip leaves
+    // both parts as register values; it combines the heads of its other
+    // lanes itself): CRC = ~step^(-8e)(step^(1024 m) tail ^ head), tables read
+    // from global memory
     if (a.span_rec) {
         const uint32_t ns = a.span_ctl[2];
-        for (uint32_t g = 1u + blockIdx.x * kBlockThreads + threadIdx.x; g < ns; g += gridDim.x * kBlockThreads) {
+        for (uint32_t g = 64u * (1u + blockIdx.x * kBlockThreads + threadIdx.x); g < ns;
+             g += 64u * gridDim.x * kBlockThreads) {
             const uint4 h = a.span_rec[g];
             if (!(h.z & kSpanHeadBit) || h.y >= a.n) continue;
             const uint32_t m = h.z & 0xFFu, e = (h.z >> 8) & 0xFFu;

@@ -83,10 +83,11 @@ __device__ LNL_INLINE SpanGeo geometry_of(const SpanArgs& a) {
     return span_geometry(b + a.off[0], b + a.off[a.n], a.waves);
 }
 
-// ceil(P / (128 R)) for a byte offset P from S0
+// ceil(P / (128 R)) for a byte offset P from S0 (lines < 2^32 whenever the
+// kernel runs: span_runs caps the batch at 64 W 8 segments of <= 127 lines)
 __device__ LNL_INLINE uint32_t seg_ceil(uint64_t P, uint32_t R) {
-    const uint64_t lines = (P + 127u) >> 7;
-    return (uint32_t)((lines + R - 1u) / R);
+    const uint32_t lines = (uint32_t)((P + 127u) >> 7);
+    return (lines + R - 1u) / R;
 }
 
 // ---- pre-pass ---------------------------------------------------------------
@@ -104,15 +105,16 @@ __device__ LNL_INLINE void append(uint32_t* cnt, uint32_t* list, bool take, uint
 
 // One thread per datagram: first[g] = min{ i : P_{i+1} > g Sb } for the g in
 // [ceil(P_i / Sb), ceil(P_{i+1} / Sb)) (first[NS] = n); CRC 0 for empty
-// datagrams; the overflow list; ctl[2] = segments.  A batch the kernel does not
-// take goes to the batch kernel whole.
+// datagrams; ctl[1] = 0 (the span kernel appends the overflow list), ctl[2] =
+// segments.  A batch the kernel does not take goes to the batch kernel whole.
+// (No atomics here, so the counters need no reset launch before it.)
 __global__ __launch_bounds__(256) void span_prep_kernel(SpanArgs a) {
     const uint64_t b = (uint64_t)(uintptr_t)a.base - a.off0;
     const SpanGeo G = geometry_of(a);
     const bool whole = !span_runs(G, a.waves);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ctl[1] = whole ? a.n : 0u;
         a.ctl[2] = whole ? 0u : G.NS;
-        if (whole) a.ctl[1] = a.n;
     }
     const uint32_t stride = gridDim.x * 256u;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
@@ -122,7 +124,6 @@ __global__ __launch_bounds__(256) void span_prep_kernel(SpanArgs a) {
         }
         const uint64_t Pi = b + a.off[i] - G.S0, Pj = b + a.off[i + 1] - G.S0;
         if (Pi == Pj) a.out[i] = 0u;  // CRC-32C of zero bytes
-        append(&a.ctl[1], a.ovf, Pj > Pi && span_overflow(Pi, Pj, G.R), i);
         const uint32_t lo = i == 0 ? 0u : seg_ceil(Pi, G.R), hi = seg_ceil(Pj, G.R);
         for (uint32_t g = lo; g < hi; ++g) a.first[g] = i;
         if (i + 1u == a.n) a.first[G.NS] = a.n;
@@ -323,6 +324,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         {
             const int64_t d0 = k0 < n ? (int64_t)(bsh + A.off[k0]) - (int64_t)segbase : 0;
             cs = d0 < -(int64_t)(2u * Sb + 2u) ? -(int32_t)(2u * Sb + 2u) : (int32_t)d0;
+            // the overflow list (datagrams touching three or more segments,
+            // span_overflow): each has exactly one segment that no datagram
+            // ends in and that it entered from the previous segment
+            append(&A.ctl[1], A.ovf, live && k0 == k1 && k0 < n && d0 < 0 && d0 >= -(int64_t)Sb, k0);
             // 16 boundaries, loaded together (indices clamped, values selected;
             // the empty asm keeps the compiler from sinking each load into its
             // own branch, which would wait for them one by one)
@@ -592,7 +597,17 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 tdone = true;
             }
         }
-        if (live)
+        // heads: CRC = ~step^(-8e)(step^(1024 m) tail ^ head), the tail from
+        // the previous lane; lane 0's from the previous wave-batch, so its
+        // record goes to the batch kernel's prologue
+        {
+            const uint32_t tprev = (uint32_t)__shfl((int)r_tail, (int)(lane - 1u) & 63, 64);
+            if (htrack && lane != 0u && hk < n) {
+                const uint32_t m = hinfo & 0xFFu, e = (hinfo >> 8) & 0xFFu;
+                A.out[hk] = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tprev) ^ r_head);
+            }
+        }
+        if (live && (lane == 0u || lane == 63u))
             A.rec[g] = make_uint4(r_head, hk, hinfo | (htrack ? kSpanHeadBit : 0u) | (ttrack ? kSpanTailBit : 0u),
                                   r_tail);
     }
@@ -618,8 +633,6 @@ void span_scratch_layout(SpanArgs& a, uint32_t* s) {
 }
 
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(a.ctl, 0, 4 * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
     const uint32_t blocks = (a.n + 255u) / 256u;
     const uint32_t prep = blocks < 8192u ? blocks : 8192u;
     hipLaunchKernelGGL(span_prep_kernel, dim3(prep), dim3(256), 0, stream, a);
