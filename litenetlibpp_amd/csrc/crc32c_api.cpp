@@ -59,7 +59,7 @@ struct DeviceState {
     uint8_t* dummy = nullptr;  // 256 zero bytes of device memory
     uint32_t* fold = nullptr;  // kernel tables (lnl_build_tables), 12.5 KiB
     uint32_t* pow = nullptr;   // segment kernel's row-power tables (lnl_build_seg_tables), 3.5 KiB
-    uint32_t* span_tab = nullptr;  // span kernel's tables (lnl_build_span_tables), 20.5 KiB
+    uint32_t* span_tab = nullptr;  // span kernel's tables (lnl_build_span_tables), 145 KiB
     int cus = 0;
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)

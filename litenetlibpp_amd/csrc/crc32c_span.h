@@ -17,9 +17,8 @@
 namespace lnl {
 
 constexpr uint32_t kSpanRmin = 16;
-constexpr uint32_t kSpanRmax = 127;      // boundaries fit 16 bits (2 Sb < 65535); A^m, m < 128
+constexpr uint32_t kSpanRmax = 127;      // boundaries fit 16 bits (2 Sb < 65535); row powers m < 128
 constexpr uint32_t kSpanMaxRounds = 8;   // wave-batches per resident wave
-constexpr uint32_t kSpanPowTables = 7;   // A^(2^b), b = 0..6 (lnl_build_seg_tables)
 
 struct SpanGeo {
     uint64_t S0;   // address of the stream's first line
@@ -62,13 +61,14 @@ LNL_HD LNL_INLINE bool span_overflow(uint64_t Pi, uint64_t Pj, uint32_t R) {
 
 // Per-segment record the kernel leaves for the fix-up: the head (the datagram
 // that entered from the previous segment and ends here) and the tail (the one
-// still open at the segment's end, ending in the next segment), folded.
-//   x: fold of the head's part in this segment   y: the head's datagram index
+// still open at the segment's end, ending in the next segment), as CRC
+// register values (lnl_span_phi below).
+//   x: the head's part in this segment   y: the head's datagram index
 //   z: m | e << 8 | head tracked << 16 | tail tracked << 17
 //      (m = rows from the segment start through the head's last row, e = bytes
 //      of that row after the head's last byte)
-//   w: fold of the tail's part in this segment
-// Head CRC = ~F_e(A^m (w of segment g-1) ^ x).
+//   w: the tail's part in this segment
+// Head CRC = ~step^(-8e)(step^(1024 m)(w of segment g-1) ^ x).
 constexpr uint32_t kSpanHeadBit = 1u << 16;
 constexpr uint32_t kSpanTailBit = 1u << 17;
 
@@ -88,16 +88,38 @@ constexpr uint32_t kSpanTailBit = 1u << 17;
 //   TB    [b] = step^(-8 b), b = 0..15 (nibble tables)
 //   TA    [a] = step^(-128 a), a = 0..7
 //   C     [pad] = step^(-8 pad)(0xFFFFFFFF)
-//   POW   [b] = step^(1024 * 2^b), b = 0..kSpanPowTables-1 (the fix-up's row
-//         powers, register basis; global memory only)
+//   ROWS  [m] = step^(1024 m), m = 0..127 (the head combine's row powers)
+//   FIN   [e] = step^(-8 e), e = 0..127 (the final map in one product)
+//   (ROWS and FIN: global memory only; one nibble-table product each, so a
+//   head costs two dependent lookups rounds, not nine)
 constexpr uint32_t kSpanTabT = 0;
 constexpr uint32_t kSpanTabS = 1024;
 constexpr uint32_t kSpanTabB = kSpanTabS + 128;
 constexpr uint32_t kSpanTabA = kSpanTabB + 16 * 128;
 constexpr uint32_t kSpanTabC = kSpanTabA + 8 * 128;
 constexpr uint32_t kSpanTabLds = kSpanTabC + 128;
-constexpr uint32_t kSpanTabPow = kSpanTabLds;
-constexpr uint32_t kSpanTabWords = kSpanTabPow + kSpanPowTables * 128;
+constexpr uint32_t kSpanTabRows = kSpanTabLds;
+constexpr uint32_t kSpanTabFin = kSpanTabRows + 128 * 128;
+constexpr uint32_t kSpanTabWords = kSpanTabFin + 128 * 128;
+
+// nibble tables (128 words) of the matrix with columns cols
+LNL_HD inline void lnl_nibble_tables(uint32_t* dst, const uint32_t* cols) {
+    for (uint32_t k = 0; k < 8; ++k)
+        for (uint32_t v = 0; v < 16; ++v) dst[16 * k + v] = lnl_cols_apply(cols, v << (4 * k));
+}
+// dst[m] = nibble tables of step^(n m), m = 0..127
+LNL_HD inline void lnl_power_tables(uint32_t* dst, int32_t n) {
+    uint32_t one[32], cur[32], nxt[32];
+    for (int k = 0; k < 32; ++k) {
+        one[k] = lnl_step_bits(1u << k, n);
+        cur[k] = 1u << k;
+    }
+    for (uint32_t m = 0; m < 128; ++m) {
+        lnl_nibble_tables(dst + 128 * m, cur);
+        for (int k = 0; k < 32; ++k) nxt[k] = lnl_cols_apply(one, cur[k]);
+        for (int k = 0; k < 32; ++k) cur[k] = nxt[k];
+    }
+}
 
 LNL_HD inline void lnl_build_span_tables(uint32_t* t) {
     for (uint32_t i = 0; i < 4; ++i)
@@ -108,10 +130,10 @@ LNL_HD inline void lnl_build_span_tables(uint32_t* t) {
             t[kSpanTabS + 16 * k + v] = lnl_step_bits(x, 256);
             for (int32_t b = 0; b < 16; ++b) t[kSpanTabB + 128 * b + 16 * k + v] = lnl_step_bits(x, -8 * b);
             for (int32_t a = 0; a < 8; ++a) t[kSpanTabA + 128 * a + 16 * k + v] = lnl_step_bits(x, -128 * a);
-            for (uint32_t b = 0; b < kSpanPowTables; ++b)
-                t[kSpanTabPow + 128 * b + 16 * k + v] = lnl_step_bits(x, (int32_t)(1024u << b));
         }
     for (uint32_t pad = 0; pad < 128; ++pad) t[kSpanTabC + pad] = lnl_step_bits(0xFFFFFFFFu, -8 * (int32_t)pad);
+    lnl_power_tables(t + kSpanTabRows, 1024);
+    lnl_power_tables(t + kSpanTabFin, -8);
 }
 
 // Host / emulation form of the fold (the kernel reads the same tables from LDS).
@@ -127,17 +149,19 @@ LNL_HD inline uint32_t lnl_span_phi(const uint32_t* t, const uint32_t* v) {
     return p;
 }
 // CRC of a datagram from its register value r (lnl_span_phi of its ended
-// state) and e, the bytes of its last row after it
-LNL_HD LNL_INLINE uint32_t lnl_span_final(const uint32_t* t, uint32_t e, uint32_t r) {
+// state) and e < 128, the bytes of its last row after it: ~step^(-8e)(r) --
+// as the kernel's LDS tables do it (TB, TA) and in one product (FIN)
+LNL_HD LNL_INLINE uint32_t lnl_span_final2(const uint32_t* t, uint32_t e, uint32_t r) {
     r = lnl_table_apply(t + kSpanTabB + 128u * (e & 15u), r);
     r = lnl_table_apply(t + kSpanTabA + 128u * (e >> 4), r);
     return ~r;
 }
-// step^(1024 m) r: m rows of zeros after a register value r (m < 2^kSpanPowTables)
+LNL_HD LNL_INLINE uint32_t lnl_span_final(const uint32_t* t, uint32_t e, uint32_t r) {
+    return ~lnl_table_apply(t + kSpanTabFin + 128u * e, r);
+}
+// step^(1024 m) r: m < 128 rows of zeros after a register value r
 LNL_HD LNL_INLINE uint32_t lnl_span_rows(const uint32_t* t, uint32_t m, uint32_t r) {
-    for (uint32_t b = 0; b < kSpanPowTables; ++b)
-        if ((m >> b) & 1u) r = lnl_table_apply(t + kSpanTabPow + 128u * b, r);
-    return r;
+    return lnl_table_apply(t + kSpanTabRows + 128u * m, r);
 }
 
 }  // namespace lnl

@@ -61,6 +61,9 @@ constexpr uint32_t kEntry = 144;   // stash entry stride: 128 B of state + 16 B 
                                    // consecutive slots start on different banks and the 8
                                    // pieces of an entry sit at immediate offsets
 constexpr uint32_t kImageBytes = 8192;
+#ifndef LNL_SPAN_PRIO
+#define LNL_SPAN_PRIO 0  // 0: progress-based issue priority; 1: static (experiment); 2: none
+#endif
 constexpr uint32_t kTabBytes = kSpanTabLds * 4;
 // LDS (bytes): the fold tables (crc32c_span.h) first -- the Horner's byte
 // lookups then address them with a 16-bit immediate offset -- and a zero
@@ -72,7 +75,8 @@ constexpr uint32_t kImageOff = (kZeroOff + 16u + 127u) & ~127u;
 constexpr uint32_t kStashOff = kImageOff + kWaves * kImageBytes;
 constexpr uint32_t kStashBytes = kCap * kEntry;
 constexpr uint32_t kMetaOff = kStashOff + kWaves * kStashBytes;
-constexpr uint32_t kLdsBytes = kMetaOff + kWaves * kCap * 8;
+constexpr uint32_t kProgOff = kMetaOff + kWaves * kCap * 8;  // rows done per wave (issue fairness)
+constexpr uint32_t kLdsBytes = kProgOff + kWaves * 4;
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
 static_assert(kTabBytes % 16 == 0 && kStashOff % 16 == 0 && kMetaOff % 8 == 0, "LDS alignment");
 
@@ -102,6 +106,8 @@ __device__ LNL_INLINE void append(uint32_t* cnt, uint32_t* list, bool take, uint
     base = (uint32_t)__shfl((int)base, (int)leader, 64);
     if (take) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = value;
 }
+
+__device__ LNL_INLINE uint32_t clamp16(int64_t v) { return v <= 0 ? 0u : (v >= 0xFFFF ? 0xFFFFu : (uint32_t)v); }
 
 // One thread per datagram: first[g] = min{ i : P_{i+1} > g Sb } for the g in
 // [ceil(P_i / Sb), ceil(P_{i+1} / Sb)) (first[NS] = n); CRC 0 for empty
@@ -146,8 +152,6 @@ struct Queue {
 };
 
 __device__ constexpr uint32_t kZero32[32] = {0u};
-
-__device__ LNL_INLINE uint32_t clamp16(int64_t v) { return v <= 0 ? 0u : (v >= 0xFFFF ? 0xFFFFu : (uint32_t)v); }
 
 // ~step^(-8e)(r): the final map (two nibble-table products, LDS)
 __device__ LNL_INLINE uint32_t final_crc_lds(uint32_t tab_base, uint32_t e, uint32_t r) {
@@ -214,6 +218,35 @@ __device__ LNL_INLINE void ds_read8(uint32_t base, uint32_t* x) {
     }
 }
 
+// read_row (crc32c_device.h) plus a ninth piece at pa, same round trip
+__device__ LNL_INLINE void read_row_pre(const uint32_t* ad, uint32_t pa, uint32_t* x, u32x4& pre) {
+    uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+    u32x4 v8;
+    asm volatile(
+        "ds_read_b128 %0, %9\n\t"
+        "ds_read_b128 %1, %10\n\t"
+        "ds_read_b128 %2, %11\n\t"
+        "ds_read_b128 %3, %12\n\t"
+        "ds_read_b128 %4, %13\n\t"
+        "ds_read_b128 %5, %14\n\t"
+        "ds_read_b128 %6, %15\n\t"
+        "ds_read_b128 %7, %16\n\t"
+        "ds_read_b128 %8, %17\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(v4), "=&v"(v5), "=&v"(v6), "=&v"(v7), "=&v"(v8)
+        : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(pa)
+        : "memory");
+    const uint4 v[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        x[4 * k + 0] = v[k].x;
+        x[4 * k + 1] = v[k].y;
+        x[4 * k + 2] = v[k].z;
+        x[4 * k + 3] = v[k].w;
+    }
+    pre = v8;
+}
+
 template <int P>
 struct Pieces {  // the 8 pieces of a 32-word state written at base + 16 p
     __device__ static LNL_INLINE void write(uint32_t base, const uint32_t* x, const uint32_t* y) {
@@ -255,22 +288,48 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
     const uint32_t stash = lds0 + kStashOff + wave * kStashBytes;
     const uint32_t meta = lds0 + kMetaOff + wave * (kCap * 8u);
     const uint32_t* const ctab = reinterpret_cast<const uint32_t*>(lds + kTabOff) + kSpanTabC;  // C[pad]
+    uint32_t* const prog = reinterpret_cast<uint32_t*>(lds + kProgOff);
+    uint32_t rows_done = 0;  // rows this wave has streamed (all its wave-batches)
 
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 16)
+    // diagnostic build only: per-wave timeline (s_memrealtime, 100 MHz) into
+    // out[8 w ..] instead of CRCs
+    uint32_t tl[5];
+    tl[0] = (uint32_t)wall_clock64();
+#define LNL_TL(i) tl[i] = (uint32_t)wall_clock64()
+#else
+#define LNL_TL(i) (void)0
+#endif
     const uint64_t bsh = (uint64_t)(uintptr_t)A.base - A.off0;
     const SpanGeo G = geometry_of(A);
     if (!span_runs(G, A.waves)) return;
     const uint32_t R = G.R, Sb = R << 7, NS = G.NS, nwb = G.nwb;
     if (blockIdx.x * kWaves >= nwb) return;  // whole workgroup idle (before the barrier)
+    const uint32_t gw = blockIdx.x * kWaves + wave;
+    const uint32_t nw = gridDim.x * kWaves;
+    const uint32_t n = A.n;
+    // the lane's first[] pair for wave-batch wb, fetched ahead (the first one
+    // before the tables go to LDS)
+    uint32_t su_k0, su_k1;
+    auto fetch = [&](uint32_t wb) {
+        const uint32_t g = wb * 64u + lane;
+        const bool ok = wb < nwb && g < NS;
+        su_k0 = ok ? A.first[g] : n;
+        su_k1 = ok ? A.first[g + 1u] : n;
+    };
+    fetch(gw);
     {
         const uint4* f = reinterpret_cast<const uint4*>(A.tab);
         uint4* fl = reinterpret_cast<uint4*>(lds + kTabOff);
         for (uint32_t i = threadIdx.x; i < kTabBytes / 16u; i += kThreads) fl[i] = f[i];
         if (threadIdx.x == 0) *reinterpret_cast<uint4*>(lds + kZeroOff) = make_uint4(0u, 0u, 0u, 0u);
+        if (threadIdx.x < (uint32_t)kWaves) prog[threadIdx.x] = 0u;
         __syncthreads();
     }
-    const uint32_t gw = blockIdx.x * kWaves + wave;
-    const uint32_t nw = gridDim.x * kWaves;
-    const uint32_t n = A.n;
+    LNL_TL(1);
+#if LNL_SPAN_PRIO == 1
+    if (wave >= 4u) __builtin_amdgcn_s_setprio(1);  // experiment: static priority for the younger waves
+#endif
 
     // per-lane addressing: load i brings piece pc of the row of lane 8 i + sub;
     // it lands in the image at that lane's row, slot pc ^ swz(8 i + sub)
@@ -315,35 +374,36 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         const uint32_t g = wb * 64u + lane;
         const bool live = g < NS;
         const uint64_t segbase = line0 + (uint64_t)lane * Sb;
-        const uint32_t k0 = live ? A.first[g] : n;
-        const uint32_t k1 = live ? A.first[g + 1u] : n;  // [k0, k1): datagrams ending in this segment
+        const uint32_t k0 = su_k0;
+        const uint32_t k1 = su_k1;  // [k0, k1): datagrams ending in this segment
         Queue Q;
         uint32_t k = k0, kq, qn;
         int32_t cs;  // first byte of datagram k, from the segment's first byte
         uint32_t inj = 0u;
         {
-            const int64_t d0 = k0 < n ? (int64_t)(bsh + A.off[k0]) - (int64_t)segbase : 0;
+            // the datagram's start and the next 16 boundaries, loaded together
+            // (indices clamped, values selected; the empty asm keeps the
+            // compiler from sinking each load into its own branch, which would
+            // wait for them one by one)
+            uint64_t ov[17];
+#pragma unroll
+            for (int j = 0; j < 17; ++j) {
+                const uint32_t kk = k0 + (uint32_t)j;
+                ov[j] = A.off[kk < n ? kk : n];
+            }
+#pragma unroll
+            for (int j = 0; j < 17; ++j) asm volatile("" : "+v"(ov[j]));
+            const int64_t d0 = k0 < n ? (int64_t)(bsh + ov[0]) - (int64_t)segbase : 0;
             cs = d0 < -(int64_t)(2u * Sb + 2u) ? -(int32_t)(2u * Sb + 2u) : (int32_t)d0;
             // the overflow list (datagrams touching three or more segments,
             // span_overflow): each has exactly one segment that no datagram
             // ends in and that it entered from the previous segment
             append(&A.ctl[1], A.ovf, live && k0 == k1 && k0 < n && d0 < 0 && d0 >= -(int64_t)Sb, k0);
-            // 16 boundaries, loaded together (indices clamped, values selected;
-            // the empty asm keeps the compiler from sinking each load into its
-            // own branch, which would wait for them one by one)
-            uint64_t ov[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t kk = k0 + (uint32_t)j + 1u;
-                ov[j] = A.off[kk < n ? kk : n];
-            }
-#pragma unroll
-            for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(ov[j]));
             uint32_t qp[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint32_t lo = clamp16((int64_t)(bsh + ov[2 * j]) - (int64_t)segbase);
-                const uint32_t hi = clamp16((int64_t)(bsh + ov[2 * j + 1]) - (int64_t)segbase);
+                const uint32_t lo = clamp16((int64_t)(bsh + ov[2 * j + 1]) - (int64_t)segbase);
+                const uint32_t hi = clamp16((int64_t)(bsh + ov[2 * j + 2]) - (int64_t)segbase);
                 const uint32_t vlo = k0 + 2u * j < n ? lo : 0xFFFFu, vhi = k0 + 2u * j + 1u < n ? hi : 0xFFFFu;
                 qp[j] = vlo | (vhi << 16);
             }
@@ -462,7 +522,8 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // stash when it is tracked (take) -- and the next one starts at b
         // with state F(b) ^ C[b].  F(b) = the row from byte b on: b's piece
         // AND-masked in place in the image, earlier pieces from a zero piece.
-        auto boundary = [&](uint32_t t, bool ev, bool zero, uint32_t b, bool take, uint32_t* sout) {
+        // (pre: the lane's piece b >> 4 as read with the row, or null: read here)
+        auto boundary = [&](uint32_t t, bool ev, bool zero, uint32_t b, bool take, uint32_t* sout, const u32x4* pre) {
             {
                 const uint32_t nst = (uint32_t)__popcll(__ballot(take));
                 const uint32_t cnt = st_tail - st_head;
@@ -476,7 +537,16 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint64_t lo = d < 8u ? ~0ull << (8u * d) : 0ull;
                 const uint64_t hi = d < 8u ? ~0ull : ~0ull << (8u * (d - 8u));
                 const uint32_t m[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-                patch_piece<0>(r0 ^ (16u * (b >> 4)), m);
+                if (pre) {
+                    u32x4 v = *pre;
+                    v.x &= m[0];
+                    v.y &= m[1];
+                    v.z &= m[2];
+                    v.w &= m[3];
+                    lds_write_piece(r0 ^ (16u * (b >> 4)), v);
+                } else {
+                    patch_piece<0>(r0 ^ (16u * (b >> 4)), m);
+                }
             }
             uint32_t F[32];
             {
@@ -526,28 +596,46 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             Transpose<0>::write(we, wo, cur);
             if (t + 2u < R) issue(t + 2u, cur);
+#if LNL_SPAN_PRIO == 0
+            // Issue fairness.  The two waves of a SIMD (wave, wave ^ 4) tie on
+            // most issue slots, and ties go to the older wave: left alone, one
+            // finishes its rows ~20 % after the other, with the SIMD half idle
+            // meanwhile.  The wave that is ahead yields (priority 0), the one
+            // behind takes priority 2.
+            {
+                ++rows_done;
+                prog[wave] = rows_done;
+                const uint32_t other = uni(prog[wave ^ 4u]);
+                if (rows_done > other)
+                    __builtin_amdgcn_s_setprio(0);
+                else
+                    __builtin_amdgcn_s_setprio(2);
+            }
+#endif
+            const uint32_t rowst = t << 7, rowend = rowst + 128u;
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 2)
+            bool ev = false;  // diagnostic build only: rows and networks, no datagram boundaries
+#else
+            bool ev = is_open() && Q.front() <= rowend;
+#endif
+            const uint32_t b = ev ? Q.front() - rowst : 128u;
+            u32x4 pre;  // the piece holding b, read with the row (no separate round trip to mask it)
             {
                 uint32_t x[32], rad[8], rr = r0;
                 asm volatile("" : "+v"(rr));  // 7 XORs per row rather than 8 registers held
 #pragma unroll
                 for (int p = 0; p < 8; ++p) rad[p] = rr ^ (16u * p);
-                read_row<0>(rad, x);
+                read_row_pre(rad, rr ^ (16u * ((b >> 4) & 7u)), x, pre);
                 lnl_net_row_x(sin, x, sout);
             }
             sout[0] ^= inj;
             inj = 0u;
-            const uint32_t rowst = t << 7, rowend = rowst + 128u;
-#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 2)
-            return;  // diagnostic build only: rows and networks, no datagram boundaries
-#endif
-            bool ev = is_open() && Q.front() <= rowend;
             if (!__any(ev)) return;
             // the first boundary of every lane (straight-line; rows with two or
             // more boundaries in one lane loop below)
             {
-                const uint32_t b = ev ? Q.front() - rowst : 128u;
                 const bool take = ev && cs >= -(int32_t)Sb;  // (a row's first boundary never ends an empty datagram)
-                boundary(t, ev, false, b, take, sout);
+                boundary(t, ev, false, b, take, sout, &pre);
             }
             refill();
             ev = is_open() && Q.front() <= rowend;
@@ -555,7 +643,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint32_t b = ev ? Q.front() - rowst : 128u;
                 const bool zero = ev && cs == (int32_t)(rowst + b);  // empty datagram (CRC written by the pre-pass)
                 const bool take = ev && !zero;                     // (started in this row: never a head)
-                boundary(t, ev, zero, b, take, sout);
+                boundary(t, ev, zero, b, take, sout, nullptr);
                 refill();
                 ev = is_open() && Q.front() <= rowend;
             }
@@ -564,6 +652,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         uint32_t sA[32], sB[32];
 #pragma unroll
         for (int w = 0; w < 32; ++w) sA[w] = 0u;
+        LNL_TL(2);
         for (uint32_t t = 0; t < R; t += 2u) {
             row_step(t, ra, sA, sB);
             if (t + 1u < R)
@@ -574,6 +663,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             }
         }
 
+        LNL_TL(3);
         // ---- the tail: the datagram still open, if it started here and ends
         // in the next segment; then fold everything still waiting -----------
         refill();
@@ -610,7 +700,17 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         if (live && (lane == 0u || lane == 63u))
             A.rec[g] = make_uint4(r_head, hk, hinfo | (htrack ? kSpanHeadBit : 0u) | (ttrack ? kSpanTailBit : 0u),
                                   r_tail);
+        fetch(wb + nw);
     }
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 16)
+    LNL_TL(4);
+    if (lane < 5u && 8u * gw + 8u <= n) {
+        uint32_t v = tl[0];
+#pragma unroll
+        for (int i = 1; i < 5; ++i) v = lane == (uint32_t)i ? tl[i] : v;
+        A.out[8u * gw + lane] = v;
+    }
+#endif
 }
 
 }  // namespace

@@ -1,6 +1,6 @@
 // Host-side check of the span kernel's fold tables (litenetlibpp_amd/csrc/crc32c_span.h):
 // the table Horner (lnl_span_phi) followed by the register-basis final map
-// (lnl_span_final) equals the bit-sliced fold (lnl_fold_tree) followed by the
+// (lnl_span_final, and the LDS form lnl_span_final2) equals the bit-sliced fold (lnl_fold_tree) followed by the
 // batch kernels' final map, for random states and every e; the row powers
 // equal step^(1024 m); and on real rows the Horner is the raw CRC of the row.
 //
@@ -37,13 +37,14 @@ int main() {
             uint32_t o = lnl_table_apply(g_tab + 128 * lnl_table_b(e), r_old);
             o = ~lnl_table_apply(g_tab + 128 * lnl_table_a(e), o);
             const uint32_t n = lnl_span_final(g_span, e, r_new);
+            const uint32_t n2 = lnl_span_final2(g_span, e, r_new);
             ++checked;
-            if (o != n) {
+            if (o != n || o != n2) {
                 if (bad < 10) printf("state %d e %u: fold tree %08x, span %08x\n", it, e, o, n);
                 ++bad;
             }
         }
-        const uint32_t m = (uint32_t)(rng() % 128);
+        const uint32_t m = it < 128 ? (uint32_t)it : (uint32_t)(rng() % 128);
         ++checked;
         if (lnl_span_rows(g_span, m, r_new) != lnl_step_bits(r_new, 1024 * (int32_t)m)) {
             if (bad < 10) printf("row power m=%u wrong\n", m);

@@ -23,6 +23,12 @@ VARIANTS = {
     "base": "",                                     # shipped: lane-run kernel for fixed strides
     "span_nofold": "-DLNL_SPAN_DIAG=1",             # CSR span kernel without its folds (wrong CRCs)
     "span_noev": "-DLNL_SPAN_DIAG=2",               # CSR span kernel: rows + network only (wrong CRCs)
+    "span_prev": ("", None, "build/span_prev.hip"),  # A/B: the span kernel source saved in build/ (untracked)
+    "span_noprio": "-DLNL_SPAN_PRIO=2",            # span kernel: no issue-priority balancing
+    "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
+    "span_timeline": "-DLNL_SPAN_DIAG=16",          # span kernel: per-wave timeline into out[] (wrong CRCs)
+    "span_noflush": "-DLNL_SPAN_DIAG=4",            # CSR span kernel: stash entries dropped unread (wrong CRCs)
+    "span_noput": "-DLNL_SPAN_DIAG=12",             # ... and not written either (wrong CRCs)
     "bucketed": ("", 4),                            # CSR: the bucketed batch kernel (previous default)
     "batch": "-DLNL_NO_RUN",                        # any-layout batch kernel for everything
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
@@ -68,13 +74,20 @@ VARIANTS = {
 
 def flags_path(v):
     """VARIANTS entry -> (extra -D flags, CSR path or None)."""
-    return (v, None) if isinstance(v, str) else v
+    return (v, None) if isinstance(v, str) else v[:2]
+
+
+def span_src(v):
+    """Optional third field: another span-kernel source (an A/B copy of an
+    earlier version, outside the tree's sources), relative to litenetlibpp_amd/."""
+    return v[2] if isinstance(v, tuple) and len(v) > 2 else "csrc/crc32c_span.hip"
 
 
 def build(names):
     for n in names:
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "litenetlibpp_amd"), "variant",
-                        f"NAME={n}", f"VFLAGS={flags_path(VARIANTS[n])[0]}"], check=True)
+                        f"NAME={n}", f"VFLAGS={flags_path(VARIANTS[n])[0]}",
+                        f"SPAN_SRC={span_src(VARIANTS[n])}"], check=True)
         print("built", n)
 
 
