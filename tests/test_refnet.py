@@ -1,0 +1,117 @@
+"""Config 1 / SURVEY 8(f)1 on the REFERENCE itself: its net_manager, compiled
+from /root/reference/src where it lies (oracle/refnet/build.py), with the
+INTEGRATION.md edits applied at link time (sendto / recvfrom wrapped by the
+product's CPU layer) and at compile time (POSSIBLE_MTU - 4 at the three sites
+that turn an MTU index into an MTU).  Runs in the build container only: the GPU
+box has no /root/reference, so everything here skips there.
+
+* should_connect_ipv4 / should_send_and_receive, recreated without gtest
+  (/root/reference/tests/net_manager_tests.cpp:6-138), CRC on and off.
+* The reference example's traffic (example/client.cpp:14-47 against
+  example/server.cpp's echo): all 25 typed messages over the five delivery
+  methods and the 13,218-byte fragment come back -- in-process, and with the
+  example's own two executables.
+* The MTU probe (net_peer.cpp:664-698) settles at 1428 with the layer (its
+  1432-byte wire datagram fits MAX_PACKET_SIZE), at 1424 when the MTU table is
+  left alone (the 1436-byte probe is truncated and dropped), at 1432 without
+  the layer.
+* A link that corrupts one datagram in five: the layer drops every corrupted
+  one (counted) and RELIABLE_ORDERED still delivers all 300 messages in order.
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.environ.get("LNL_REFERENCE", "/root/reference")
+NET = os.path.join(ROOT, "oracle", "_ref", "net")
+LIB = os.path.join(ROOT, "litenetlibpp_amd", "liblnl_crc32c.so")
+
+pytestmark = pytest.mark.skipif(
+    not os.path.isdir(os.path.join(REF, "src")) or shutil.which("g++") is None or not os.path.exists(LIB),
+    reason="needs /root/reference, g++ and the built library (build container only)")
+
+
+@pytest.fixture(scope="module")
+def built():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "refnet", "build.py")],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return NET
+
+
+def drive(built, variant, *args, timeout=120):
+    exe = os.path.join(built, variant, "refnet_driver")
+    r = subprocess.run([exe] + list(args), capture_output=True, text=True, timeout=timeout)
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert line, r.stdout + r.stderr
+    res = json.loads(line[-1])
+    assert r.returncode == 0 and res["ok"], res
+    return res
+
+
+@pytest.mark.parametrize("variant", ["crc", "plain"])
+@pytest.mark.parametrize("test", ["connect", "send_receive"])
+def test_reference_tests_recreated(built, variant, test):
+    res = drive(built, variant, test)
+    assert res["crc"] == (variant == "crc")
+    assert res["dropped"] == 0
+
+
+@pytest.mark.parametrize("variant", ["crc", "plain"])
+def test_reference_example_echo(built, variant):
+    res = drive(built, variant, "echo")
+    assert res["typed_echoed"] == 25 and res["fragment_echoed"] == 1
+
+
+def test_reference_example_processes(built):
+    """The example's own executables (crc variant): the client prints 25 CNT
+    lines and the fragment check (example/client.cpp:60-71)."""
+    d = os.path.join(built, "crc")
+    lb = ["stdbuf", "-oL"] if shutil.which("stdbuf") else []  # both poll forever: line-buffer what they print
+    srv = subprocess.Popen(lb + [os.path.join(d, "lnl_example_server")], stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True)
+    try:
+        time.sleep(0.5)
+        cli = subprocess.Popen(lb + [os.path.join(d, "lnl_example_client")], stdout=subprocess.PIPE,
+                               stderr=subprocess.STDOUT, text=True)
+        try:
+            out, _ = cli.communicate(timeout=4)
+        except subprocess.TimeoutExpired:
+            cli.kill()  # the example client polls forever
+            out, _ = cli.communicate()
+    finally:
+        srv.kill()
+        srv.communicate()
+    cnt = [l for l in out.splitlines() if l.startswith("CNT:")]
+    assert len(cnt) == 25, out
+    kinds = {tuple(int(x.split(":")[1]) for x in l.split(",")[1:3]) for l in cnt}
+    assert kinds == {(t, i) for t in range(5) for i in range(5)}, out
+    assert "TestFrag: 192, 31" in out, out
+
+
+@pytest.mark.parametrize("variant,mtu", [("crc", 1428), ("crc_nomtu", 1424), ("plain", 1432)])
+def test_mtu_probe_settles(built, variant, mtu):
+    res = drive(built, variant, "mtu", timeout=60)
+    assert res["mtu"] == mtu, res
+    assert res["max_wire"] <= res["max_packet_size"] == 1432
+    if variant == "crc_nomtu":
+        assert res["dropped"] > 0  # the truncated 1436-byte probes
+
+
+def test_bit_flipping_link(built):
+    res = drive(built, "crc", "flip", "5", timeout=60)
+    assert res["received"] == 300 and res["in_order"]
+    assert res["dropped"] == res["flipped"] > 0  # every corrupted datagram, and nothing else
+
+
+def test_lossy_link_plain_reference(built):
+    """The same traffic over a lossy link without the layer: the reliable
+    channel's recovery that the flip test relies on is the reference's own."""
+    res = drive(built, "plain", "lose", "5", timeout=60)
+    assert res["received"] == 300 and res["in_order"] and res["lost"] > 0
