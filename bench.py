@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "dispatch"], default="fixed",
+    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "dispatch", "append"], default="fixed",
                     help="fixed: config 2 (the headline; config 4 at N = 8); csr: config 3; filter: the "
                          "batched inbound filter (CRC check + net_packet::verify) over the config-3 batch as "
                          "wire datagrams; xor: the XOR-encryption layer in place over the config-2 batch; "
@@ -130,6 +130,10 @@ def make_workload(args, rank, world, device):
     data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=device, generator=g)
     if args.workload == "filter":  # status byte out instead of a CRC word
         return dict(data=data, n=n, L=None, off=off, payload=total, algo=total + n + 8 * (n + 1), filter=True)
+    if args.workload == "append":  # the outbound layer: payload || LE32(crc) per datagram into a wire burst
+        wire = torch.empty(total + 4 * n, dtype=torch.uint8, device=device)
+        return dict(data=data, n=n, L=None, off=off, payload=total, wire=wire, append=True,
+                    algo=total + (total + 4 * n) + 4 * n + 8 * (n + 1))
     return dict(data=data, n=n, L=None, off=off, payload=total, algo=total + 4 * n + 8 * (n + 1))
 
 
@@ -190,6 +194,10 @@ def launch(P, w, out, stream):
         P.xor_layer_fixed(w["data"], w["L"], w["L"], w["n"], XOR_KEY, stream=stream)
     elif w.get("filter"):
         P.inbound_filter(w["data"], w["off"], out=w["status"], stream=stream)
+    elif w.get("append"):  # CRCs into out (checked like csr), wire bytes into w["wire"]
+        P._lib.check(P.lib().lnl_crc32c_append_csr_dev(
+            w["data"].data_ptr(), w["off"].data_ptr(), w["n"], w["wire"].data_ptr(), out.data_ptr(),
+            stream.cuda_stream), "lnl_crc32c_append_csr_dev")
     elif w["off"] is None:
         P.batch_fixed(w["data"], w["L"], w["L"], w["n"], out=out, stream=stream)
     else:
@@ -319,7 +327,19 @@ def parity_sample(w, out, host):
         exp = oracle.batch_fixed(data, w["L"], w["L"], k)
     else:
         exp = oracle.batch_csr(data, off[: k + 1])
-    return bool(np.array_equal(got, exp)), k
+    ok = bool(np.array_equal(got, exp))
+    if ok and w.get("append"):  # the wire bytes of the same datagrams: payload || LE32(crc)
+        o = off[: k + 1].astype(np.int64)
+        lens = np.diff(o)
+        wire = w["wire"][: int(o[k] - o[0]) + 4 * k].cpu().numpy()
+        crcpos = (o[1:] - o[0]) + 4 * np.arange(1, k + 1) - 4
+        keep = np.ones(wire.size, dtype=bool)
+        for j in range(4):
+            keep[crcpos + j] = False
+        ok = (np.array_equal(wire[keep], data[o[0]:o[k]]) and
+              np.array_equal(wire[crcpos[:, None] + np.arange(4)[None, :]].reshape(-1),
+                             exp.astype("<u4").view(np.uint8)) and lens.size == k)
+    return ok, k
 
 
 def host_path_rate(P, host, w, device):
@@ -444,13 +464,16 @@ def main():
             "filter": "config-3 batch as wire datagrams through lnl_inbound_filter_csr_dev",
             "xor": "XOR layer over the config-2 batch, in place (22-byte key)",
             "dispatch": "2^20 accepted MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire), "
-                        "lnl_dispatch_csr_dev"}[args.workload]
+                        "lnl_dispatch_csr_dev",
+            "append": "config-3 batch through lnl_crc32c_append_csr_dev (outbound layer: wire burst of "
+                      "payload || LE32(crc))"}[args.workload]
         line = {
             "metric": {"fixed": METRIC,
                        "csr": "CRC32C GB/s (device-resident) over 1M mixed-length (64-1400B) packets; bit-exact",
                        "filter": "inbound filter GB/s (CRC check + verify, device-resident) over 1M mixed-length (64-1400B) datagrams",
                        "xor": "XOR-layer GB/s (device-resident, in place) over 1M x 1400B packets",
-                       "dispatch": "dispatch GB/s (MERGED containers cut on device) over 1M x 1300B datagrams"}[args.workload],
+                       "dispatch": "dispatch GB/s (MERGED containers cut on device) over 1M x 1300B datagrams",
+                       "append": "outbound-layer GB/s (CRC + append, device-resident) over 1M mixed-length (64-1400B) payloads"}[args.workload],
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,

@@ -107,6 +107,15 @@ int lnl_crc32c_batch_fixed_dev(const uint8_t* d_base, size_t stride, uint32_t le
 int lnl_crc32c_batch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
                              uint32_t* d_out, void* hip_stream);
 
+/* Batched outbound layer (the send side over a CSR burst): datagram i,
+ * d_base[d_off[i] .. d_off[i+1]), goes to d_dst + (d_off[i] - d_off[0]) + 4 i
+ * as payload || LE32(CRC32C(payload)) -- the bytes lnl_crc32c_layer_outbound
+ * gives for it -- so the wire burst is back to back, d_off[n] - d_off[0] + 4 n
+ * bytes.  d_crc (optional, may be NULL) also receives the CRCs.  d_dst must not
+ * overlap the source bytes.  Stream-ordered; returns 0 or a negative errno. */
+int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t* d_dst,
+                              uint32_t* d_crc, void* hip_stream);
+
 /* Batched inbound verification (the layer's receive side over a CSR batch of
  * whole datagrams, trailing LE32 CRC included): d_ok[i] = 1 if datagram i has
  * length >= 5 and its trailing CRC matches, else 0.  d_crc (optional, may be

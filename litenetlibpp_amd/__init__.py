@@ -8,6 +8,7 @@ from .crc32c import (  # noqa: F401
     EXTRA_PACKET_SIZE,
     Crc32cError,
     Crc32cLayer,
+    append_csr,
     batch_csr,
     batch_fixed,
     batch_host,

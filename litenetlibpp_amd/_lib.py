@@ -51,6 +51,8 @@ def lib() -> ctypes.CDLL:
     L.lnl_crc32c_batch_csr_dev.restype = ctypes.c_int
     L.lnl_crc32c_batch_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p,
                                            ctypes.c_void_p]
+    L.lnl_crc32c_append_csr_dev.restype = ctypes.c_int
+    L.lnl_crc32c_append_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, ctypes.c_void_p]
     L.lnl_crc32c_verify_csr_dev.restype = ctypes.c_int
     L.lnl_crc32c_verify_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p,
                                             ctypes.c_void_p]

@@ -170,6 +170,30 @@ def batch_csr(data, offsets, out=None, stream=None):
     return out
 
 
+def append_csr(data, offsets, out=None, want_crc: bool = False, stream=None):
+    """Batched outbound layer: the wire burst of a CSR burst of payloads --
+    datagram i at (off[i] - off[0]) + 4 i as payload || LE32(crc) (what
+    lnl_crc32c_layer_outbound writes for it).  Returns the uint8 wire tensor
+    (off[n] - off[0] + 4 n bytes; ``out`` may supply it) [, crc (int32)]."""
+    torch = _torch()
+    _check_dev_u8(data, "data")
+    _check_off(offsets, data)
+    n = offsets.numel() - 1
+    size = int(offsets[-1].item() - offsets[0].item()) + 4 * n if n > 0 else 0
+    if out is None:
+        out = torch.empty(size, dtype=torch.uint8, device=data.device)
+    else:
+        _check_dev_u8(out, "out")
+        if out.numel() < size:
+            raise ValueError(f"out holds {out.numel()} bytes, the wire burst needs {size}")
+    crc = torch.empty(max(n, 0), dtype=torch.int32, device=data.device) if want_crc else None
+    if n > 0:
+        check(lib().lnl_crc32c_append_csr_dev(data.data_ptr(), offsets.data_ptr(), n, out.data_ptr(),
+                                              crc.data_ptr() if crc is not None else None,
+                                              _stream_handle(stream)), "lnl_crc32c_append_csr_dev")
+    return (out, crc) if want_crc else out
+
+
 def verify_csr(data, offsets, want_crc: bool = False, stream=None):
     """Batched inbound layer: ok[i] = datagram i (trailing LE32 CRC included)
     is >= 5 bytes and its CRC matches.  Returns ok (uint8) [, crc (int32)]."""

@@ -490,6 +490,39 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
                uint32_t filter, void* hip_stream);
 }  // namespace
 
+// The outbound layer over a device burst: the CSR CRC pass (into d_crc, or
+// stream-ordered scratch), then the append kernel (lnl_append.hip).
+extern "C" int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t* d_dst,
+                                         uint32_t* d_crc, void* hip_stream) {
+    if (n == 0) return 0;
+    if (!d_off || !d_dst) return fail(-EINVAL, "d_off / d_dst is NULL");
+    if (!d_base) return fail(-EINVAL, "d_base is NULL");
+    DeviceState* S;
+    if (int rc = current_device(&S)) return rc;
+    const hipStream_t st = (hipStream_t)hip_stream;
+    uint32_t* crc = d_crc;
+    if (!crc) {
+        hipError_t e = hipMallocAsync((void**)&crc, (size_t)n * sizeof(uint32_t), st);
+        if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", (size_t)n * 4, hipGetErrorString(e));
+    }
+    lnl::BatchArgs a{};
+    a.base = d_base;
+    a.off = d_off;
+    a.n = n;
+    a.out = crc;
+    int rc = launch_csr(*S, a, lnl::kModeCsr, st);
+    if (rc == 0) {
+        lnl::AppendArgs p{d_base, d_off, n, d_dst, crc};
+        hipError_t e = lnl::launch_append(p, S->cus, st);
+        if (e != hipSuccess) rc = hip_fail(e, "append kernel launch");
+    }
+    if (!d_crc) {
+        hipError_t e = hipFreeAsync(crc, st);
+        if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    }
+    return rc;
+}
+
 extern "C" int lnl_crc32c_verify_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
                                          uint8_t* d_ok, uint32_t* d_crc, void* hip_stream) {
     return verify_csr(d_base, d_off, n, d_ok, d_crc, 0u, hip_stream);

@@ -181,6 +181,17 @@ size_t span_scratch_words(uint32_t n, uint32_t waves);
 void span_scratch_layout(SpanArgs& a, uint32_t* scratch);
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream);
 
+// Outbound layer over a device burst (lnl_append.hip): datagram i of the CSR
+// burst to dst + (off[i] - off[0]) + 4 i as payload || LE32(crc[i]).
+struct AppendArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    uint32_t n;
+    uint8_t* dst;
+    const uint32_t* crc;
+};
+hipError_t launch_append(const AppendArgs& a, int cus, hipStream_t stream);
+
 // CSR uniform path (crc32c_csr.hip): plan pre-pass + uniform line-count
 // batches that fetch each shared boundary line once.  The caller then runs
 // the batch kernel over ovf (perm_n = ctl + 1) with tail_xor = tail.

@@ -709,3 +709,58 @@ def test_full_config3_survey_recipe(P):
     exp = oracle.batch_csr(host, off)
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+
+
+# ---- outbound layer over a device burst (lnl_crc32c_append_csr_dev) ----------
+@pytest.mark.parametrize("case", ["mixed", "tiny_and_empty", "long"])
+def test_append_csr_matches_layer_outbound(P, case):
+    """Every byte of the wire burst equals lnl_crc32c_layer_outbound (the CPU
+    layer, called per datagram through the C ABI) of each payload, back to
+    back; the CRCs equal the oracle's; nothing outside the burst is written
+    (guard bytes around an unaligned destination)."""
+    rng = np.random.default_rng(["mixed", "tiny_and_empty", "long"].index(case) + 900)
+    n = {"mixed": 20000, "tiny_and_empty": 30000, "long": 600}[case]
+    if case == "mixed":
+        lens = rng.integers(0, 1501, n)
+    elif case == "tiny_and_empty":
+        lens = np.where(rng.random(n) < 0.3, 0, rng.integers(1, 40, n))
+    else:
+        lens = rng.integers(2000, 40000, n)
+    lead = int(rng.integers(0, 128))
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(lead)
+    data = rng.integers(0, 256, int(off[-1]) + 5, dtype=np.uint8)
+    size = int(off[-1] - off[0]) + 4 * n
+    shift = int(rng.integers(1, 16))
+    buf = torch.full((size + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    wire, crc = P.append_csr(dev(data), dev(off.view(np.int64), torch.int64), out=buf[shift:shift + size],
+                             want_crc=True)
+    assert np.array_equal(u32(crc), oracle.batch_csr(data, off))
+    got = buf.cpu().numpy()
+    assert (got[:shift] == 0xA5).all() and (got[shift + size:] == 0xA5).all(), "wrote outside the burst"
+    layer = P.Crc32cLayer()
+    exp = b"".join(layer.process_outbound(data, int(off[i]), int(lens[i])) for i in range(n))
+    assert got[shift:shift + size].tobytes() == exp
+
+
+def test_append_csr_config3_full(P):
+    """2^20 config-3 payloads (SURVEY recipe shape): CRCs bit-exact and the
+    first 50,000 datagrams' wire bytes exact; every CRC field holds its CRC."""
+    rng = np.random.default_rng(77)
+    n = 1 << 20
+    lens = rng.integers(64, 1401, n)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(78)
+    d = torch.randint(0, 256, (int(off[-1]),), dtype=torch.uint8, device="cuda", generator=g)
+    wire, crc = P.append_csr(d, dev(off.view(np.int64), torch.int64), want_crc=True)
+    data = d.cpu().numpy()
+    exp_crc = oracle.batch_csr(data, off)
+    assert np.array_equal(u32(crc), exp_crc)
+    w = wire.cpu().numpy()
+    crcpos = off[1:].astype(np.int64) + 4 * np.arange(n)
+    fields = w[crcpos[:, None] + np.arange(4)[None, :]].reshape(-1).view("<u4")
+    assert np.array_equal(fields, exp_crc)
+    k = 50000
+    keep = np.ones(int(off[k]) + 4 * k, dtype=bool)
+    keep[(crcpos[:k, None] + np.arange(4)[None, :]).reshape(-1)] = False
+    assert np.array_equal(w[: keep.size][keep], data[: int(off[k])])
