@@ -31,7 +31,7 @@ Variants:
   crc_nomtu  the layer on, MTU table untouched (negative control: the 1432
              probe no longer fits and the MTU settles one step lower)
 
-Usage: python3 oracle/refnet/build.py [variant ...]   (default: all three)
+Usage: python3 oracle/refnet/build.py [--if-stale] [variant ...]   (default: all three)
 """
 import os
 import re
@@ -109,14 +109,30 @@ def build(variant):
     return sites
 
 
+def stale(variant):
+    """True when a variant's driver is missing or older than anything it is built from."""
+    exe = os.path.join(OUT, variant, "refnet_driver")
+    if not os.path.exists(exe):
+        return True
+    t = os.path.getmtime(exe)
+    deps = lib_sources() + [os.path.join(HERE, f) for f in ("build.py", "refnet_wrap.cpp", "refnet_driver.cpp")]
+    deps += [os.path.join(LIBDIR, "liblnl_crc32c.so"), os.path.join(REPO, "include", "lnl_crc32c.h")]
+    return any(os.path.getmtime(f) > t for f in deps)
+
+
 def main():
+    args = [a for a in sys.argv[1:] if a != "--if-stale"]
+    only_stale = "--if-stale" in sys.argv[1:]
     if not os.path.isdir(os.path.join(REF, "src")):
         print(f"no reference at {REF}: nothing to build", file=sys.stderr)
         return 1
     if not os.path.exists(os.path.join(LIBDIR, "liblnl_crc32c.so")):
         print("build litenetlibpp_amd/liblnl_crc32c.so first (make -C litenetlibpp_amd)", file=sys.stderr)
         return 1
-    for v in sys.argv[1:] or ["plain", "crc", "crc_nomtu"]:
+    for v in args or ["plain", "crc", "crc_nomtu"]:
+        if only_stale and not stale(v):
+            print(v, "up to date")
+            continue
         sites = build(v)
         print(v, "built; MTU sites rewritten:", sum(sites.values()))
     return 0
