@@ -322,8 +322,12 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 // once, one 512-thread workgroup per CU) after its pre-pass, then the batch
 // kernel, which completes the cross-segment heads and takes the datagrams the
 // span kernel leaves (three or more segments; device-side count).
-int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
+// (span_mode: kSpanCrc -> out[i]; kSpanVerify / kSpanFilter -> ok[i], the
+// overflow datagrams through the batch kernel in verify mode)
+int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st, uint32_t span_mode = lnl::kSpanCrc) {
     lnl::SpanArgs g{};
+    g.mode = span_mode;
+    g.ok = a.ok;
     g.base = a.base;
     g.off = a.off;
     g.off0 = a.off0;
@@ -346,7 +350,8 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
         o.span_rec = g.rec;
         o.span_ctl = g.ctl;
         o.span_tab = S.span_tab;
-        rc = launch(S, o, lnl::kModeCsr, st);
+        o.span_thdr = g.thdr;
+        rc = launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st);
     }
     e = hipFreeAsync(scratch, st);
     if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
@@ -550,6 +555,11 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
     a.filter = filter;
     hipStream_t st = (hipStream_t)hip_stream;
     const int path = csr_path();
+    // large batches, status only: the span kernel (every line read once), the
+    // whole datagram's CRC against the residue; with body CRCs wanted (d_crc)
+    // the bucketed batch kernel, which computes them
+    if (n >= LNL_BUCKET_MIN_N && !d_crc && path == kPathBucketed)
+        return launch_csr_span(*S, a, st, filter ? lnl::kSpanFilter : lnl::kSpanVerify);
     if (n < LNL_BUCKET_MIN_N || path == kPathBucketed || path == kPathBucketCsr)
         return launch_csr(*S, a, lnl::kModeVerify, st);
 #if !LNL_EXPERIMENTS

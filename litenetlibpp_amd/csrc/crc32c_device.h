@@ -20,6 +20,15 @@ __device__ LNL_INLINE uint32_t swz(uint32_t row) { return (row >> 1) & 7u; }
 
 __device__ LNL_INLINE uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// A global-address-space view of an integer address: a plain pointer made from
+// an integer would compile to flat instructions.  (The host pass only parses
+// device code.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LNL_GLOBAL(T, a) reinterpret_cast<__attribute__((address_space(1))) T*>(a)
+#else
+#define LNL_GLOBAL(T, a) reinterpret_cast<T*>(a)
+#endif
+
 // One LDS word read in inline asm (see read_row for why asm).
 __device__ LNL_INLINE uint32_t lds_read_u32(uint32_t addr) {
     uint32_t v;

@@ -32,7 +32,8 @@ struct BatchArgs {
     // optional (CSR span path): the span kernel's per-segment head / tail
     // records, completed first (crc32c_span.h); span_ctl[2] = segments
     const uint4* span_rec;
-    const uint32_t* span_ctl;
+    const uint32_t* span_ctl;   // [2] segments, [3] lines per segment
+    const uint8_t* span_thdr;   // verify modes: header byte of each segment's tail datagram
     const uint32_t* span_tab;  // kSpanTabWords words (lnl_build_span_tables)
 };
 
@@ -176,6 +177,11 @@ struct SpanArgs {
     uint32_t* first;         // span_max_segments(waves) + 1
     uint32_t* ovf;           // n: datagrams left to the batch kernel
     uint4* rec;              // span_max_segments(waves) head / tail records
+    // verify modes (kSpanVerify, kSpanFilter): ok[i] instead of out[i]; thdr:
+    // per segment, the header byte of its tail datagram
+    uint32_t mode;
+    uint8_t* ok;
+    uint8_t* thdr;
 };
 size_t span_scratch_words(uint32_t n, uint32_t waves);
 void span_scratch_layout(SpanArgs& a, uint32_t* scratch);

@@ -277,13 +277,21 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
     // lanes itself): CRC = ~step^(-8e)(step^(1024 m) tail ^ head), tables read
     // from global memory
     if (a.span_rec) {
-        const uint32_t ns = a.span_ctl[2];
+        const uint32_t ns = a.span_ctl[2], Sb = a.span_ctl[3] << 7;
         for (uint32_t g = 64u * (1u + blockIdx.x * kBlockThreads + threadIdx.x); g < ns;
              g += 64u * gridDim.x * kBlockThreads) {
             const uint4 h = a.span_rec[g];
             if (!(h.z & kSpanHeadBit) || h.y >= a.n) continue;
             const uint32_t m = h.z & 0xFFu, e = (h.z >> 8) & 0xFFu;
-            a.out[h.y] = lnl_span_final(a.span_tab, e, lnl_span_rows(a.span_tab, m, a.span_rec[g - 1u].w) ^ h.x);
+            const uint4 tr = a.span_rec[g - 1u];
+            const uint32_t crc = lnl_span_final(a.span_tab, e, lnl_span_rows(a.span_tab, m, tr.w) ^ h.x);
+            if constexpr (kMode == kModeVerify) {  // the whole datagram's CRC against the residue
+                const uint32_t len = (Sb - (tr.z >> kSpanTailShift)) + (m << 7) - e;
+                a.ok[h.y] = (uint8_t)lnl_span_status(a.filter ? kSpanFilter : kSpanVerify, crc, len,
+                                                     a.span_thdr[g - 1u]);
+            } else {
+                a.out[h.y] = crc;
+            }
         }
     }
     // entries to process: n, or a device-side count of perm entries

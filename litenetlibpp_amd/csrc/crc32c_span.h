@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include "crc32c_bitslice.h"
+#include "lnl_packet.h"
 
 namespace lnl {
 
@@ -71,6 +72,18 @@ LNL_HD LNL_INLINE bool span_overflow(uint64_t Pi, uint64_t Pj, uint32_t R) {
 // Head CRC = ~step^(-8e)(step^(1024 m)(w of segment g-1) ^ x).
 constexpr uint32_t kSpanHeadBit = 1u << 16;
 constexpr uint32_t kSpanTailBit = 1u << 17;
+// z >> kSpanTailShift: where the tail datagram starts, bytes from the segment's
+// first byte (< Sb <= 16,256: 14 bits)
+constexpr uint32_t kSpanTailShift = 18;
+
+// ---- verify modes ---------------------------------------------------------------
+// The span kernel checks a wire datagram (payload || LE32(CRC)) without
+// locating its CRC field: CRC-32C over the WHOLE datagram is the residue
+// 0x48674BC7 exactly when the trailing four bytes are the CRC of the rest (the
+// CRC of m || t is a bijection of t, and t = CRC(m) gives the residue).  So a
+// verify call computes the same whole-datagram CRCs as a CSR call and compares.
+enum : uint32_t { kSpanCrc = 0, kSpanVerify = 1, kSpanFilter = 2 };
+constexpr uint32_t kCrc32cResidue = 0x48674BC7u;
 
 // ---- the span kernel's fold -------------------------------------------------
 // A state V (32 words) is folded to the CRC register directly: L(fold(V)) (the
@@ -162,6 +175,15 @@ LNL_HD LNL_INLINE uint32_t lnl_span_final(const uint32_t* t, uint32_t e, uint32_
 // step^(1024 m) r: m < 128 rows of zeros after a register value r
 LNL_HD LNL_INLINE uint32_t lnl_span_rows(const uint32_t* t, uint32_t m, uint32_t r) {
     return lnl_table_apply(t + kSpanTabRows + 128u * m, r);
+}
+
+// LNL_INBOUND_* of a wire datagram from its whole-datagram CRC, its length and
+// its first byte (verify: 1 / 0 only; filter: then net_packet::verify() of the
+// stripped packet, lnl_packet.h)
+LNL_HD LNL_INLINE uint32_t lnl_span_status(uint32_t mode, uint32_t crc, uint32_t len, uint32_t hdr) {
+    if (len < 5u || crc != kCrc32cResidue) return 0u;
+    if (mode != kSpanFilter) return 1u;
+    return lnl_packet_verify_hdr((uint8_t)hdr, len - 4u) ? 1u : 2u;
 }
 
 }  // namespace lnl

@@ -121,6 +121,7 @@ __global__ __launch_bounds__(256) void span_prep_kernel(SpanArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctl[1] = whole ? a.n : 0u;
         a.ctl[2] = whole ? 0u : G.NS;
+        a.ctl[3] = G.R;
     }
     const uint32_t stride = gridDim.x * 256u;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
@@ -129,7 +130,12 @@ __global__ __launch_bounds__(256) void span_prep_kernel(SpanArgs a) {
             continue;
         }
         const uint64_t Pi = b + a.off[i] - G.S0, Pj = b + a.off[i + 1] - G.S0;
-        if (Pi == Pj) a.out[i] = 0u;  // CRC-32C of zero bytes
+        if (Pi == Pj) {  // CRC-32C of zero bytes; a datagram too short for the layer
+            if (a.mode == kSpanCrc)
+                a.out[i] = 0u;
+            else
+                a.ok[i] = 0u;
+        }
         const uint32_t lo = i == 0 ? 0u : seg_ceil(Pi, G.R), hi = seg_ceil(Pj, G.R);
         for (uint32_t g = lo; g < hi; ++g) a.first[g] = i;
         if (i + 1u == a.n) a.first[G.NS] = a.n;
@@ -152,6 +158,20 @@ struct Queue {
 };
 
 __device__ constexpr uint32_t kZero32[32] = {0u};
+
+// byte b & 15 of a 16-byte piece held in registers
+__device__ LNL_INLINE uint32_t piece_byte(const u32x4& v, uint32_t b) {
+    const uint32_t w = (b >> 2) & 3u;
+    const uint32_t x = w == 0u ? v.x : (w == 1u ? v.y : (w == 2u ? v.z : v.w));
+    return (x >> (8u * (b & 3u))) & 0xFFu;
+}
+
+// one LDS byte (asm, with its wait: see read_row)
+__device__ LNL_INLINE uint32_t lds_read_u8(uint32_t addr) {
+    uint32_t v;
+    asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
 
 // ~step^(-8e)(r): the final map (two nibble-table products, LDS)
 __device__ LNL_INLINE uint32_t final_crc_lds(uint32_t tab_base, uint32_t e, uint32_t r) {
@@ -380,6 +400,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         uint32_t k = k0, kq, qn;
         int32_t cs;  // first byte of datagram k, from the segment's first byte
         uint32_t inj = 0u;
+        // verify modes: header byte of datagram k (when it started here); taken
+        // from the next row's byte 0 when it starts on a row boundary
+        uint32_t chdr = 0u;
+        bool hdr_next = false;
         {
             // the datagram's start and the next 16 boundaries, loaded together
             // (indices clamped, values selected; the empty asm keeps the
@@ -421,6 +445,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 cs = -(int32_t)(2u * Sb + 2u);
             } else if (k0 < n && cs == 0) {
                 inj = 0xFFFFFFFFu;  // C[0]: datagram k0 starts at row 0, byte 0
+                hdr_next = true;
             }
         }
         // k0 < n: the lane has a datagram open (k0 - 1 when virtual)
@@ -455,7 +480,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 
         // ---- stash (wave-uniform counters) ---------------------------------
         uint32_t st_head = 0, st_tail = 0, head_slot = 0, tail_slot = 0;
-        uint32_t hpos = 0, tpos = 0, r_head = 0, r_tail = 0, hk = 0, hinfo = 0;
+        uint32_t hpos = 0, tpos = 0, r_head = 0, r_tail = 0, hk = 0, hinfo = 0, tcs = 0, thdr = 0;
         bool hpend = false, tpend = false, htrack = false, ttrack = false;
 
         // Fold the nf oldest entries, one per lane.  The caller's live state
@@ -477,9 +502,14 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 #else
             const uint32_t r = phi_lds(T, tab_base, v);
 #endif
-            const uint32_t type = (mt.y >> 8) & 3u, e = mt.y & 127u;
+            const uint32_t type = (mt.y >> 8) & 3u, e = mt.y & 127u;  // mt.y: e | type << 8 | hdr << 10 | len << 18
             const uint32_t crc = final_crc_lds(tab_base, e, r);
-            if (act && type == kTypeNormal && mt.x < n) A.out[mt.x] = crc;  // (the index check only guards the store)
+            if (act && type == kTypeNormal && mt.x < n) {  // (the index check only guards the store)
+                if (A.mode == kSpanCrc)
+                    A.out[mt.x] = crc;
+                else
+                    A.ok[mt.x] = (uint8_t)lnl_span_status(A.mode, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
+            }
             // head / tail folds back to the lanes that own them
             const uint32_t hs = hpos - st_head, ts = tpos - st_head;
             const uint32_t rh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (hs & 63u)), (int)r);
@@ -557,7 +587,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 read_row<0>(ad, F);
             }
             const bool head = cs < 0;
-            const uint32_t pos = put(take, sout, F, (128u - b) | ((head ? kTypeHead : kTypeNormal) << 8));
+            // (a normal datagram started in this segment: len < Sb < 2^14)
+            const uint32_t len = head ? 0u : (t << 7) + b - (uint32_t)cs;
+            const uint32_t pos = put(take, sout, F,
+                                     (128u - b) | ((head ? kTypeHead : kTypeNormal) << 8) | (chdr << 10) | (len << 18));
             if (take && head) {
                 hpos = pos;
                 hpend = true;
@@ -573,6 +606,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             if (start) {
                 cs = (int32_t)((t << 7) + b);
                 inj = b == 128u ? 0xFFFFFFFFu : 0u;  // C[0] at the next row's word 0
+                if (A.mode != kSpanCrc) {  // the new datagram's first byte (intact after the patch)
+                    hdr_next = b == 128u;
+                    if (b < 128u) chdr = pre ? piece_byte(*pre, b) : lds_read_u8((r0 ^ (16u * (b >> 4))) + (b & 15u));
+                }
             }
 #pragma unroll
             for (int w = 0; w < 32; ++w) sout[w] = start ? F[w] : sout[w];
@@ -626,6 +663,8 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 #pragma unroll
                 for (int p = 0; p < 8; ++p) rad[p] = rr ^ (16u * p);
                 read_row_pre(rad, rr ^ (16u * ((b >> 4) & 7u)), x, pre);
+                if (hdr_next) chdr = x[0] & 0xFFu;  // a datagram that started at this row's byte 0
+                hdr_next = false;
                 lnl_net_row_x(sin, x, sout);
             }
             sout[0] ^= inj;
@@ -683,6 +722,8 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     tpos = pos;
                     tpend = true;
                     ttrack = true;
+                    tcs = (uint32_t)cs;
+                    thdr = chdr;
                 }
                 tdone = true;
             }
@@ -691,15 +732,26 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // the previous lane; lane 0's from the previous wave-batch, so its
         // record goes to the batch kernel's prologue
         {
-            const uint32_t tprev = (uint32_t)__shfl((int)r_tail, (int)(lane - 1u) & 63, 64);
+            const int src = (int)(lane - 1u) & 63;
+            const uint32_t tprev = (uint32_t)__shfl((int)r_tail, src, 64);
+            const uint32_t tcs_prev = (uint32_t)__shfl((int)tcs, src, 64);
+            const uint32_t thdr_prev = (uint32_t)__shfl((int)thdr, src, 64);
             if (htrack && lane != 0u && hk < n) {
                 const uint32_t m = hinfo & 0xFFu, e = (hinfo >> 8) & 0xFFu;
-                A.out[hk] = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tprev) ^ r_head);
+                const uint32_t crc = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tprev) ^ r_head);
+                if (A.mode == kSpanCrc)
+                    A.out[hk] = crc;
+                else  // the head's length: its part in the previous segment and in this one
+                    A.ok[hk] = (uint8_t)lnl_span_status(A.mode, crc, (Sb - tcs_prev) + (m << 7) - e, thdr_prev);
             }
         }
-        if (live && (lane == 0u || lane == 63u))
-            A.rec[g] = make_uint4(r_head, hk, hinfo | (htrack ? kSpanHeadBit : 0u) | (ttrack ? kSpanTailBit : 0u),
+        if (live && (lane == 0u || lane == 63u)) {
+            A.rec[g] = make_uint4(r_head, hk,
+                                  hinfo | (htrack ? kSpanHeadBit : 0u) | (ttrack ? kSpanTailBit : 0u) |
+                                      (tcs << kSpanTailShift),
                                   r_tail);
+            if (A.mode != kSpanCrc) A.thdr[g] = (uint8_t)thdr;
+        }
         fetch(wb + nw);
     }
 #if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 16)
@@ -719,7 +771,7 @@ size_t span_scratch_words(uint32_t n, uint32_t waves) {
     const size_t ns = span_max_segments(waves);
     size_t w = 4 + (ns + 1) + n;
     w = (w + 3) & ~(size_t)3;  // rec[] is 16-byte aligned
-    return w + 4 * ns;
+    return w + 4 * ns + (ns + 3) / 4;  // + thdr[ns]
 }
 
 void span_scratch_layout(SpanArgs& a, uint32_t* s) {
@@ -730,6 +782,7 @@ void span_scratch_layout(SpanArgs& a, uint32_t* s) {
     size_t w = 4 + (ns + 1) + a.n;
     w = (w + 3) & ~(size_t)3;
     a.rec = reinterpret_cast<uint4*>(s + w);
+    a.thdr = reinterpret_cast<uint8_t*>(a.rec + ns);
 }
 
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc32c_device.h"
 #include "crc32c_kernels.h"
 
 namespace lnl {
@@ -34,13 +35,7 @@ struct __attribute__((packed, aligned(4))) U4a {  // 16 bytes at a 4-byte aligne
     uint32_t x, y, z, w;
 };
 
-// global-address-space views of an address (plain pointers made from integers
-// would compile to flat instructions; the host pass only parses this code)
-#if defined(__HIP_DEVICE_COMPILE__)
-#define LNL_G(T, a) reinterpret_cast<__attribute__((address_space(1))) T*>(a)
-#else
-#define LNL_G(T, a) reinterpret_cast<T*>(a)
-#endif
+#define LNL_G LNL_GLOBAL  // crc32c_device.h
 
 __device__ inline uint8_t out_byte(uint64_t x, uint64_t P1, uint64_t delta, uint32_t crc) {
     return x < P1 ? *LNL_G(const uint8_t, x - delta) : (uint8_t)(crc >> (8u * (uint32_t)(x - P1)));

@@ -27,6 +27,8 @@ VARIANTS = {
     "span_noprio": "-DLNL_SPAN_PRIO=2",            # span kernel: no issue-priority balancing
     "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
     "span_timeline": "-DLNL_SPAN_DIAG=16",          # span kernel: per-wave timeline into out[] (wrong CRCs)
+    "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
+    "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
     "app_t64": "-DLNL_APPEND_TEAM=64",              # append kernel: 64 lanes per datagram (default 32)
     "span_noflush": "-DLNL_SPAN_DIAG=4",            # CSR span kernel: stash entries dropped unread (wrong CRCs)
     "span_noput": "-DLNL_SPAN_DIAG=12",             # ... and not written either (wrong CRCs)
@@ -136,6 +138,21 @@ def run(names, rounds, workloads):
 
             def call(L):
                 L.lnl_crc32c_batch_csr_dev(data.data_ptr(), off.data_ptr(), n_pk, out.data_ptr(), s.cuda_stream)
+        elif wl[0] == "filter":  # ("filter", n, lmin, lmax): inbound filter over a CSR burst (random bytes)
+            _, n_pk, lmin, lmax = wl
+            lens = torch.randint(lmin, lmax + 1, (n_pk,), device=dev, generator=g, dtype=torch.int64)
+            off = torch.zeros(n_pk + 1, dtype=torch.int64, device=dev)
+            off[1:] = torch.cumsum(lens, 0)
+            total = int(off[-1])
+            data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+            st = torch.empty(n_pk, dtype=torch.uint8, device=dev)
+            algo = total + n_pk + 8 * (n_pk + 1)
+            wkey = f"filter{n_pk}x{lmin}-{lmax}"
+
+            def call(L):
+                L.lnl_inbound_filter_csr_dev(ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()),
+                                             ctypes.c_uint32(n_pk), ctypes.c_void_p(st.data_ptr()),
+                                             ctypes.c_void_p(s.cuda_stream))
         elif wl[0] == "append":  # ("append", n, lmin, lmax): the outbound layer over a CSR burst
             _, n_pk, lmin, lmax = wl
             lens = torch.randint(lmin, lmax + 1, (n_pk,), device=dev, generator=g, dtype=torch.int64)
@@ -198,7 +215,7 @@ def main():
     if a.cmd == "build":
         build(names)
     else:
-        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.split(":")[0] in ("csr", "xor", "append")
+        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.split(":")[0] in ("csr", "xor", "append", "filter")
               else tuple(int(v) for v in w.split(":")) for w in a.workloads.split(",")]
         res = run(names, a.rounds, wl)
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
