@@ -112,3 +112,16 @@ def test_survey_config3_recipe_pin():
     for kind in KINDS:
         assert oracle.crc(b, kind) == pin["out0"]
     assert recipe_pins()["config2"]["out0"] == 0xD26C5CFE
+
+
+def test_crc32c_residue():
+    """CRC-32C over m || LE32(CRC-32C(m)) is the residue 0x48674BC7 for every
+    m (the span kernel's verify test, crc32c_span.h kCrc32cResidue), and any
+    other trailing value misses it."""
+    import struct
+    rng = np.random.default_rng(31)
+    for n in list(range(0, 40)) + [127, 128, 129, 1400, 1432]:
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        c = oracle.crc(m)
+        assert oracle.crc(m + struct.pack("<I", c)) == 0x48674BC7
+        assert oracle.crc(m + struct.pack("<I", c ^ (1 << int(rng.integers(0, 32))))) != 0x48674BC7
