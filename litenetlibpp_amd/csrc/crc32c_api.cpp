@@ -462,7 +462,7 @@ extern "C" int lnl_crc32c_batch_fixed_dev(const uint8_t* d_base, size_t stride, 
         r.base = d_base;
         r.out = d_out;
         r.fold = S->fold;
-        hipError_t e = lnl::launch_crc32c_run(r, grid_for_waves(*S, r.nb), st);
+        hipError_t e = lnl::launch_crc32c_run(r, grid_for_waves(*S, r.nb, lnl::kRunThreads), st);
         if (e != hipSuccess) return hip_fail(e, "kernel launch");
         if (n_main == n) return 0;
     }

@@ -8,6 +8,12 @@ namespace lnl {
 
 constexpr int kBlockThreads = 256;  // 4 waves; 64 KiB LDS -> 2 workgroups per CU
 constexpr int kWavesPerCU = 8;
+// the lane-run kernel's workgroup (crc32c_run.hip): 256 threads, two per CU,
+// or 512 (one per CU, its 8 waves sharing LDS progress words for issue fairness)
+#ifndef LNL_RUN_THREADS
+#define LNL_RUN_THREADS 256
+#endif
+constexpr int kRunThreads = LNL_RUN_THREADS;
 
 enum : int { kModeFixed = 0, kModeCsr = 1, kModeVerify = 2 };
 

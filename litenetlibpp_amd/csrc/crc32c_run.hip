@@ -46,8 +46,14 @@ namespace {
 
 using namespace dev;
 
-constexpr int kWaves = kBlockThreads / 64;
-constexpr int kLdsU4 = kWaves * 2 * kBufU4 + kFoldU4;
+// issue fairness between the two waves of a SIMD (needs both in one
+// workgroup: LNL_RUN_THREADS 512); see crc32c_span.hip
+#ifndef LNL_RUN_PRIO
+#define LNL_RUN_PRIO 0
+#endif
+constexpr int kWaves = kRunThreads / 64;
+constexpr int kLdsU4 = kWaves * 2 * kBufU4 + kFoldU4 + 1;  // + one uint4: per-wave progress words
+static_assert(!LNL_RUN_PRIO || kWaves == 8, "priority balancing pairs wave w with w ^ 4");
 
 // Wave-uniform description of one lane-run batch.
 struct RunBatch {
@@ -134,7 +140,7 @@ __device__ LNL_INLINE uint32_t final_map(uint32_t fold_base, uint32_t e, uint32_
     return ~r;
 }
 
-__global__ __launch_bounds__(kBlockThreads, 2) void crc32c_run_kernel(RunArgs a) {
+__global__ __launch_bounds__(kRunThreads, 512 / kRunThreads) void crc32c_run_kernel(RunArgs a) {
     __shared__ __attribute__((aligned(16))) uint4 lds[kLdsU4];
     const uint32_t lane = __lane_id();
     const uint32_t wave = uni(threadIdx.x >> 6);
@@ -143,9 +149,14 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_run_kernel(RunArgs a)
     const uint32_t fold_base = (uint32_t)(uintptr_t)fold_lds;
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.fold);
-        for (int i = threadIdx.x; i < kFoldU4; i += kBlockThreads) fold_lds[i] = g[i];
+        for (int i = threadIdx.x; i < kFoldU4; i += kRunThreads) fold_lds[i] = g[i];
+        if (threadIdx.x == 0) fold_lds[kFoldU4] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
     }
+    uint32_t* const prog = reinterpret_cast<uint32_t*>(fold_lds + kFoldU4);
+    uint32_t rows_done = 0;
+    (void)prog;
+    (void)rows_done;
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint32_t nw = gridDim.x * kWaves;
     if (gw >= a.nb) return;
@@ -210,6 +221,17 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_run_kernel(RunArgs a)
                 have1 = 1;
             }
         }
+#if LNL_RUN_PRIO
+        {  // the wave ahead of its SIMD partner yields
+            ++rows_done;
+            prog[wave & 7u] = rows_done;
+            const uint32_t other = uni(prog[(wave & 7u) ^ 4u]);
+            if (rows_done > other)
+                __builtin_amdgcn_s_setprio(0);
+            else
+                __builtin_amdgcn_s_setprio(2);
+        }
+#endif
 
         const bool st = ks < K && (sb >> 7) == t;
         const bool en = ke < K && (eb >> 7) == t;
@@ -288,7 +310,7 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_run_kernel(RunArgs a)
 }  // namespace
 
 hipError_t launch_crc32c_run(const RunArgs& a, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL(crc32c_run_kernel, dim3(grid), dim3(kBlockThreads), 0, stream, a);
+    hipLaunchKernelGGL(crc32c_run_kernel, dim3(grid), dim3(kRunThreads), 0, stream, a);
     return hipGetLastError();
 }
 

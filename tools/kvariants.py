@@ -27,6 +27,8 @@ VARIANTS = {
     "span_noprio": "-DLNL_SPAN_PRIO=2",            # span kernel: no issue-priority balancing
     "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
     "span_timeline": "-DLNL_SPAN_DIAG=16",          # span kernel: per-wave timeline into out[] (wrong CRCs)
+    "run512": "-DLNL_RUN_THREADS=512",              # lane-run kernel: one 512-thread workgroup per CU
+    "run512p": "-DLNL_RUN_THREADS=512 -DLNL_RUN_PRIO=1",  # ... with progress-based issue priority
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
     "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
     "app_t64": "-DLNL_APPEND_TEAM=64",              # append kernel: 64 lanes per datagram (default 32)
