@@ -64,12 +64,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "dispatch", "append"], default="fixed",
+    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "dispatch", "append", "filter_dispatch",
+                                           "filter_then_dispatch"], default="fixed",
                     help="fixed: config 2 (the headline; config 4 at N = 8); csr: config 3; filter: the "
                          "batched inbound filter (CRC check + net_packet::verify) over the config-3 batch as "
                          "wire datagrams; xor: the XOR-encryption layer in place over the config-2 batch; "
                          "dispatch: lnl_dispatch_csr_dev over accepted MERGED containers of 256-B "
-                         "messages (the config-1 traffic shape)")
+                         "messages (the config-1 traffic shape); filter_dispatch: the same containers as wire "
+                         "datagrams through lnl_inbound_filter_dispatch_csr_dev (one pass: the walk in the "
+                         "filter's span kernel); filter_then_dispatch: the two calls, for comparison")
     ap.add_argument("--packets", type=int, default=1 << 20, help="per GPU")
     ap.add_argument("--length", type=int, default=1400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,8 +118,14 @@ def make_workload(args, rank, world, device):
         L = args.length
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
         return dict(data=data, n=n, L=L, off=None, payload=n * L, algo=2 * n * L, xor=True)
-    if args.workload == "dispatch":
-        return make_dispatch_workload(n, device, g)
+    if args.workload in ("dispatch", "filter_dispatch", "filter_then_dispatch"):
+        w = make_dispatch_workload(n, device, g)
+        if args.workload != "dispatch":  # statuses written by the timed call; every byte read
+            w.update(dispatch=False, fused=args.workload == "filter_dispatch", filter_dispatch=True,
+                     status=torch.empty(n, dtype=torch.uint8, device=device),
+                     algo=w["payload"] + 8 * (n + 1) + n + w["pkts"] * 16)
+            w.pop("line_bytes")
+        return w
     if args.workload == "fixed":
         L = args.length
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=device, generator=g)
@@ -185,7 +194,19 @@ def make_dispatch_workload(n, device, g):
 def launch(P, w, out, stream):
     if DRY:
         return
-    if w.get("dispatch"):
+    if w.get("filter_dispatch"):
+        if w["fused"]:
+            P._lib.check(P.lib().lnl_inbound_filter_dispatch_csr_dev(
+                w["data"].data_ptr(), w["off"].data_ptr(), w["n"], w["status"].data_ptr(),
+                w["pkt_start"].data_ptr(), w["pkt_len"].data_ptr(), w["pkt_parent"].data_ptr(), w["pkts"],
+                w["total"].data_ptr(), stream.cuda_stream), "lnl_inbound_filter_dispatch_csr_dev")
+        else:
+            P.inbound_filter(w["data"], w["off"], out=w["status"], stream=stream)
+            P._lib.check(P.lib().lnl_dispatch_csr_dev(
+                w["data"].data_ptr(), w["off"].data_ptr(), w["n"], w["status"].data_ptr(),
+                w["pkt_start"].data_ptr(), w["pkt_len"].data_ptr(), w["pkt_parent"].data_ptr(), w["pkts"],
+                w["total"].data_ptr(), stream.cuda_stream), "lnl_dispatch_csr_dev")
+    elif w.get("dispatch"):
         P._lib.check(P.lib().lnl_dispatch_csr_dev(
             w["data"].data_ptr(), w["off"].data_ptr(), w["n"], w["status"].data_ptr(),
             w["pkt_start"].data_ptr(), w["pkt_len"].data_ptr(), w["pkt_parent"].data_ptr(), w["pkts"],
@@ -439,11 +460,21 @@ def main():
 
     # checker, outside the timed region: every rank compares its first
     # datagrams with the oracle (rank 0 at N = 1: the whole batch, below)
-    crc_workload = not DRY and not (w.get("xor") or w.get("filter") or w.get("dispatch"))
+    crc_workload = not DRY and not (w.get("xor") or w.get("filter") or w.get("dispatch") or w.get("filter_dispatch"))
     host = host_copy(w) if crc_workload else None
     ok_sample = 1.0
     if crc_workload:
         ok, _k = parity_sample(w, out, host)
+        ok_sample = 1.0 if ok else 0.0
+    if not DRY and w.get("filter_dispatch"):  # every container accepted and cut into its 5 packets
+        n, S = w["n"], DISPATCH_STRIDE
+        i = torch.arange(n, dtype=torch.int64, device=device)
+        j = torch.arange(DISPATCH_SUBS, dtype=torch.int64, device=device)
+        exp_start = (i[:, None] * S + 1 + j[None, :] * DISPATCH_SUB + 2).reshape(-1)
+        ok = (bool((w["status"] == 1).all()) and int(w["total"].item()) == w["pkts"]
+              and torch.equal(w["pkt_start"], exp_start)
+              and bool((w["pkt_len"] == DISPATCH_SUB - 2).all())
+              and torch.equal(w["pkt_parent"].to(torch.int64), i.repeat_interleave(DISPATCH_SUBS)))
         ok_sample = 1.0 if ok else 0.0
     ok_all = gather_over_ranks(ok_sample, red_dev)
 
@@ -465,6 +496,10 @@ def main():
             "xor": "XOR layer over the config-2 batch, in place (22-byte key)",
             "dispatch": "2^20 accepted MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire), "
                         "lnl_dispatch_csr_dev",
+            "filter_dispatch": "2^20 MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire) through "
+                               "lnl_inbound_filter_dispatch_csr_dev (filter + cut in one pass)",
+            "filter_then_dispatch": "2^20 MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire): "
+                                    "lnl_inbound_filter_csr_dev, then lnl_dispatch_csr_dev",
             "append": "config-3 batch through lnl_crc32c_append_csr_dev (outbound layer: wire burst of "
                       "payload || LE32(crc))"}[args.workload]
         line = {
@@ -473,6 +508,8 @@ def main():
                        "filter": "inbound filter GB/s (CRC check + verify, device-resident) over 1M mixed-length (64-1400B) datagrams",
                        "xor": "XOR-layer GB/s (device-resident, in place) over 1M x 1400B packets",
                        "dispatch": "dispatch GB/s (MERGED containers cut on device) over 1M x 1300B datagrams",
+                       "filter_dispatch": "filter + dispatch GB/s (CRC check, verify, MERGED cut; device-resident) over 1M x 1300B datagrams",
+                       "filter_then_dispatch": "filter + dispatch GB/s (two calls; device-resident) over 1M x 1300B datagrams",
                        "append": "outbound-layer GB/s (CRC + append, device-resident) over 1M mixed-length (64-1400B) payloads"}[args.workload],
             "value": round(value, 2),
             "unit": "GB/s",
@@ -523,6 +560,9 @@ def main():
                 line["roofline"]["measured_stream_read_peak_gbs"] = round(peak, 1)
                 line["roofline"]["measured_stream_read_forms_gbs"] = {names[k]: round(v, 1) for k, v in probe.items()}
                 line["roofline"]["frac_of_measured_peak"] = round(achieved / peak, 4)
+        if w.get("filter_dispatch"):
+            line["parity_whole_batch"] = ("exact" if min(ok_all) == 1.0 else "MISMATCH") + \
+                " (every status ACCEPT; every packet's start, length and parent as laid out)"
         if crc_workload:
             line["parity_on_sample"] = ("bit-exact" if min(ok_all) == 1.0 else "MISMATCH") + \
                 f" (first {min(w['n'], 1 << 14)} datagrams of each of {world} rank(s) vs the oracle)"

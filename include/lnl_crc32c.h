@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 6
+#define LNL_CRC32C_ABI_VERSION 7
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -149,6 +149,17 @@ int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t
 int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, const uint8_t* d_status,
                          uint64_t* d_pkt_start, uint32_t* d_pkt_len, uint32_t* d_pkt_parent, uint32_t cap,
                          uint32_t* d_total, void* hip_stream);
+
+/* lnl_inbound_filter_csr_dev followed by lnl_dispatch_csr_dev, same outputs
+ * (d_status[i] for every datagram, then the delivered packets), with the
+ * MERGED walk done in the filter's pass over the bytes: the dispatch step
+ * reads no datagram bytes again for batches the span path takes.  This is
+ * the receive_logic -> process_packet chain (net_manager.cpp:218-222 -> :343
+ * -> net_peer.cpp:164-187) for a whole burst.  Stream-ordered. */
+int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                        uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
+                                        uint32_t* d_pkt_parent, uint32_t cap, uint32_t* d_total,
+                                        void* hip_stream);
 
 /* Upstream LiteNetLib's XOR-encryption layer (XorEncryptLayer; SURVEY.md 8(f)
  * item 4), in place: data[i] ^= key[i % key_len] for i < length, the key phase

@@ -14,6 +14,7 @@ from .crc32c import (  # noqa: F401
     batch_host,
     batch_host_multi,
     dispatch,
+    filter_dispatch,
     xor_layer,
     xor_layer_csr,
     xor_layer_fixed,

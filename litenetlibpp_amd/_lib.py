@@ -74,6 +74,9 @@ def lib() -> ctypes.CDLL:
     L.lnl_dispatch_csr_dev.restype = ctypes.c_int
     L.lnl_dispatch_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, _c_u8p, _c_u8p,
                                        ctypes.c_uint32, _c_u8p, ctypes.c_void_p]
+    L.lnl_inbound_filter_dispatch_csr_dev.restype = ctypes.c_int
+    L.lnl_inbound_filter_dispatch_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, _c_u8p,
+                                                      _c_u8p, ctypes.c_uint32, _c_u8p, ctypes.c_void_p]
     L.lnl_xor_layer.restype = ctypes.c_int
     L.lnl_xor_layer.argtypes = [_c_u8p, ctypes.c_size_t, _c_u8p, ctypes.c_size_t]
     L.lnl_xor_layer_csr_dev.restype = ctypes.c_int

@@ -34,7 +34,7 @@ HEADER_SIZE = 1        # net_constants::HEADER_SIZE (/root/reference/include/lnl
 __all__ = [
     "Crc32cError", "EXTRA_PACKET_SIZE", "crc32c", "crc32c_extend", "Crc32cLayer",
     "batch_fixed", "batch_csr", "verify_csr", "batch_host", "batch_host_multi", "mtu_with_layer",
-    "packet_verify", "inbound_status", "inbound_filter", "inbound_filter_host", "ingress_recv_batch",
+    "packet_verify", "inbound_status", "inbound_filter", "filter_dispatch", "inbound_filter_host", "ingress_recv_batch",
     "dispatch", "xor_layer", "xor_layer_csr", "xor_layer_fixed",
     "INGRESS_SLOT",
     "INBOUND_DROP_CRC", "INBOUND_ACCEPT", "INBOUND_MALFORMED",
@@ -273,6 +273,40 @@ def dispatch(data, offsets, status, cap: Optional[int] = None, stream=None):
         cap = t
     k = min(t, cap)
     return start[:k], length[:k], parent[:k]
+
+
+def filter_dispatch(data, offsets, cap: Optional[int] = None, out=None, stream=None):
+    """inbound_filter + dispatch in one pass over the bytes
+    (lnl_inbound_filter_dispatch_csr_dev).  Returns (status uint8, start int64,
+    length int32, parent int32); the packets as dispatch() returns them."""
+    torch = _torch()
+    _check_dev_u8(data, "data")
+    _check_off(offsets, data)
+    n = offsets.numel() - 1
+    dev = data.device
+    status = out if out is not None else torch.empty(max(n, 0), dtype=torch.uint8, device=dev)
+    if status.dtype != torch.uint8 or status.numel() < max(n, 0) or status.device != dev \
+            or not status.is_contiguous():
+        raise ValueError("out must be a contiguous uint8 tensor of n entries on the data's device")
+    total = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def run(c):
+        start = torch.empty(max(c, 1), dtype=torch.int64, device=dev)
+        length = torch.empty(max(c, 1), dtype=torch.int32, device=dev)
+        parent = torch.empty(max(c, 1), dtype=torch.int32, device=dev)
+        check(lib().lnl_inbound_filter_dispatch_csr_dev(
+            data.data_ptr(), offsets.data_ptr(), max(n, 0), status.data_ptr(), start.data_ptr(),
+            length.data_ptr(), parent.data_ptr(), c, total.data_ptr(), _stream_handle(stream)),
+            "lnl_inbound_filter_dispatch_csr_dev")
+        return start, length, parent
+
+    start, length, parent = run(cap if cap is not None else 0)
+    t = int(total.item()) & 0xFFFFFFFF  # u32 count
+    if cap is None:
+        start, length, parent = run(t)
+        cap = t
+    k = min(t, cap)
+    return status, start[:k], length[:k], parent[:k]
 
 
 def _key(key) -> bytes:

@@ -324,9 +324,12 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 // span kernel leaves (three or more segments; device-side count).
 // (span_mode: kSpanCrc -> out[i]; kSpanVerify / kSpanFilter -> ok[i], the
 // overflow datagrams through the batch kernel in verify mode)
-int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st, uint32_t span_mode = lnl::kSpanCrc) {
+int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st, uint32_t span_mode = lnl::kSpanCrc,
+                    uint32_t* walk_counts = nullptr, uint32_t* walk_rec = nullptr) {
     lnl::SpanArgs g{};
     g.mode = span_mode;
+    g.wcnt = walk_counts;  // filter + dispatch: the MERGED walk in the same pass
+    g.wrec = walk_rec;
     g.ok = a.ok;
     g.base = a.base;
     g.off = a.off;
@@ -794,6 +797,62 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     int rc = 0;
     e = lnl::launch_dispatch(a, tmp, scan_bytes, st);
     if (e != hipSuccess) rc = hip_fail(e, "dispatch launch");
+    e = hipFreeAsync(scratch, st);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
+}
+
+// lnl_inbound_filter_csr_dev + lnl_dispatch_csr_dev in one pass over the
+// bytes: large batches walk their MERGED containers inside the span kernel
+// (crc32c_span.hip, WALK), so the dispatch step reads no datagram bytes again;
+// small ones run the two calls.
+extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                                   uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
+                                                   uint32_t* d_pkt_parent, uint32_t cap, uint32_t* d_total,
+                                                   void* hip_stream) {
+    if (!d_total) return fail(-EINVAL, "d_total is NULL");
+    hipStream_t st = (hipStream_t)hip_stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_total, 0, 4, st);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
+    if (!d_base || !d_off || !d_status) return fail(-EINVAL, "NULL argument");
+    if (cap && (!d_pkt_start || !d_pkt_len || !d_pkt_parent)) return fail(-EINVAL, "NULL output");
+    DeviceState* S;
+    if (int rc = current_device(&S)) return rc;
+    if (n < LNL_BUCKET_MIN_N || csr_path() != kPathBucketed) {
+        if (int rc = lnl_inbound_filter_csr_dev(d_base, d_off, n, d_status, hip_stream)) return rc;
+        return lnl_dispatch_csr_dev(d_base, d_off, n, d_status, d_pkt_start, d_pkt_len, d_pkt_parent, cap, d_total,
+                                    hip_stream);
+    }
+    const size_t scan_bytes = lnl::dispatch_scan_bytes(n);
+    void* scratch = nullptr;
+    const size_t bytes = (2 + (size_t)lnl::kDispatchRec) * n * 4 + scan_bytes + 256;
+    hipError_t e = hipMallocAsync(&scratch, bytes, st);
+    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
+    lnl::DispatchArgs a{};
+    a.base = d_base;
+    a.off = d_off;
+    a.n = n;
+    a.status = d_status;
+    a.counts = (uint32_t*)scratch;
+    a.first = a.counts + n;
+    a.rec = a.first + n;
+    a.pkt_start = d_pkt_start;
+    a.pkt_len = d_pkt_len;
+    a.pkt_parent = d_pkt_parent;
+    a.cap = cap;
+    a.total = d_total;
+    void* tmp = (void*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);
+    lnl::BatchArgs b{};
+    b.base = d_base;
+    b.off = d_off;
+    b.n = n;
+    b.ok = d_status;
+    b.filter = 1u;
+    int rc = launch_csr_span(*S, b, st, lnl::kSpanFilter, a.counts, a.rec);
+    if (rc == 0 && (e = lnl::launch_dispatch_walked(a, tmp, scan_bytes, st)) != hipSuccess)
+        rc = hip_fail(e, "dispatch launch");
     e = hipFreeAsync(scratch, st);
     if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
     return rc;

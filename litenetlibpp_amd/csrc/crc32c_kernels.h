@@ -188,6 +188,11 @@ struct SpanArgs {
     uint32_t mode;
     uint8_t* ok;
     uint8_t* thdr;
+    // filter + dispatch (kSpanFilter only; null otherwise): the MERGED walk of
+    // every datagram, done by the lane its first byte streams through --
+    // DispatchArgs::counts / rec layout; kWalkPending where no lane walked it
+    uint32_t* wcnt;
+    uint32_t* wrec;
 };
 size_t span_scratch_words(uint32_t n, uint32_t waves);
 void span_scratch_layout(SpanArgs& a, uint32_t* scratch);
@@ -285,8 +290,13 @@ struct DispatchArgs {
     uint32_t* total;        // device: packets delivered (may exceed cap)
 };
 constexpr uint32_t kDispatchRec = 8;  // packets per datagram kept from the counting walk
+constexpr uint32_t kWalkPending = 0xFFFFFFFFu;  // counts[i]: not walked yet (fused path)
 size_t dispatch_scan_bytes(uint32_t n);
 hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
+// Fused path (lnl_inbound_filter_dispatch_csr_dev): counts / rec already hold
+// the span kernel's walk; the fix-up zeroes the counts of datagrams not
+// accepted and walks the kWalkPending ones, then scan + emit as above.
+hipError_t launch_dispatch_walked(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
 
 // Verify epilogue (crc32c_verify.hip): ok / body CRC from wire-datagram CRCs.
 struct VerifyArgs {

@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void span_prep_kernel(SpanArgs a) {
     }
     const uint32_t stride = gridDim.x * 256u;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+        if (a.wcnt) a.wcnt[i] = kWalkPending;  // filter + dispatch: the kernel walks what it owns
         if (whole) {
             a.ovf[i] = i;
             continue;
@@ -296,6 +297,28 @@ struct Transpose<8> {
     __device__ static LNL_INLINE void write(uint32_t, uint32_t, const u32x4*) {}
 };
 
+// one byte of a 4-byte-aligned pair of dwords: bytes q[0..2] (global memory;
+// see lnl_dispatch.hip load3 for why both dwords are inside the batch)
+__device__ LNL_INLINE uint32_t global_load3(uint64_t q) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(q & ~(uint64_t)3);
+    const uint64_t v = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    return (uint32_t)(v >> ((q & 3u) * 8u));
+}
+
+constexpr uint32_t kMergedProperty = 12;  // PACKET_PROPERTY::MERGED, net_enums.h:60
+// walk flags (WALK): the open datagram started in this lane's segment (the
+// lane writes its packet count), is a MERGED container, is still being walked
+enum : uint32_t { kWalkOwned = 1, kWalkMerged = 2, kWalkOn = 4 };
+
+// WALK (filter + dispatch): besides the statuses, every datagram whose first
+// byte streams through a lane is cut as net_peer::process_packet's MERGED case
+// does (/root/reference/src/lnl/net_peer.cpp:164-187; restated in
+// lnl_dispatch.hip walk()) while its bytes sit in the lane's LDS row, so the
+// dispatch pass does not fetch the size fields again.  Entries whose three
+// bytes (u16 size, header byte) are all in the row are taken at the row; one
+// that straddles the row end keeps the row's last two bytes for the next row;
+// a container still open at the segment's end is finished from global memory.
+template <bool WALK>
 __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
     __shared__ __attribute__((aligned(128))) uint8_t lds[kLdsBytes];
     const uint32_t lane = __lane_id();
@@ -478,6 +501,106 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             }
         };
 
+        // ---- MERGED walk (WALK only) ---------------------------------------
+        // Two registers (the kernel is at the VGPR budget):
+        //   wla = wp | wc << 18: wp, the next entry's u16 size field, bytes from
+        //        the segment's first byte (< Sb + 2^16 + 2 < 2^18); wc, entries
+        //        taken (< Sb / 3 < 2^14)
+        //   wlb = wsv | wfl << 16: wsv, bytes 126, 127 of the previous row; wfl,
+        //        the walk flags
+        uint32_t wla = 0u, wlb = 0u;
+        // bytes q, q + 1, q + 2 (q >= the row's first byte - 2) of row t
+        auto walk_read3 = [&](uint32_t t, int32_t q) -> uint32_t {
+            const int32_t j = q - (int32_t)(t << 7);
+            uint32_t ad[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const uint32_t u = j + i < 0 ? 0u : (uint32_t)(j + i);
+                ad[i] = (r0 ^ (16u * (u >> 4))) + (u & 15u);
+            }
+            uint32_t v0, v1, v2;
+            asm volatile(
+                "ds_read_u8 %0, %3\n\t"
+                "ds_read_u8 %1, %4\n\t"
+                "ds_read_u8 %2, %5\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(v0), "=&v"(v1), "=&v"(v2)
+                : "v"(ad[0]), "v"(ad[1]), "v"(ad[2])
+                : "memory");
+            if (j < 0) v0 = (wlb >> (8 * (j + 2))) & 0xFFu;
+            if (j < -1) v1 = (wlb >> 8) & 0xFFu;
+            return v0 | (v1 << 8) | (v2 << 16);
+        };
+        // take the entries of the owned container (sel) whose three bytes lie
+        // before lim; size_end: the container's end without the CRC field
+        // (the walk rules of lnl_dispatch.hip walk(), segment-relative)
+        auto walk_fields = [&](uint32_t t, bool sel, int32_t size_end, int32_t lim) {
+            bool act = sel && (wlb & (kWalkOn << 16));
+            while (__any(act)) {
+                if (act) {
+                    const int32_t wp = (int32_t)(wla & 0x3FFFFu);
+                    const uint32_t wc = wla >> 18;
+                    if (wp + 2 > size_end) {
+                        wlb &= ~(kWalkOn << 16);
+                        act = false;
+                    } else if (wp + 3 > lim) {
+                        act = false;  // next row
+                    } else {
+                        const uint32_t v = walk_read3(t, wp);
+                        const int32_t L = (int32_t)(v & 0xFFFFu), p2 = wp + 2;
+                        if (L > size_end - p2 || L == 0 || !lnl_packet_verify_hdr((uint8_t)(v >> 16), (uint32_t)L)) {
+                            wlb &= ~(kWalkOn << 16);
+                            act = false;
+                        } else {
+                            if (wc < kDispatchRec) A.wrec[(size_t)wc * n + k] = ((uint32_t)(p2 - cs) << 16) | (uint32_t)L;
+                            wla = (uint32_t)(p2 + L) | ((wc + 1u) << 18);
+                        }
+                    }
+                }
+            }
+        };
+        // datagram k (owned) starts at cs with header byte chdr (k = n: the
+        // batch's last datagram has just ended, nothing opens)
+        auto walk_open = [&]() {
+            wlb = k >= n ? 0u : (kWalkOwned | ((chdr & 0x1Fu) == kMergedProperty ? (kWalkMerged | kWalkOn) : 0u)) << 16;
+            wla = (uint32_t)(cs + 1);
+        };
+        // datagram k ends, len bytes: its packet count (a plain one is one
+        // packet, the whole datagram without the CRC field)
+        auto walk_close = [&](uint32_t len) {
+            if (wlb & (kWalkOwned << 16)) {
+                if (wlb & (kWalkMerged << 16)) {
+                    A.wcnt[k] = wla >> 18;
+                } else {
+                    A.wrec[k] = len - 4u;
+                    A.wcnt[k] = 1u;
+                }
+            }
+            wlb = 0u;
+        };
+        // once row t's boundaries are done (called before row t + 1's
+        // transpose): the open container's entries in row t, and the row's
+        // last two bytes when an entry straddles into row t + 1
+        auto row_walk = [&](uint32_t t) {
+            const int32_t rowend = (int32_t)(t << 7) + 128;
+            // (a boundary clamped to 0xFFFF lies beyond the segment: no bound yet)
+            const uint32_t qf = Q.front();
+            walk_fields(t, true, qf == 0xFFFFu ? 0x7FFFFFFF : (int32_t)qf - 4, rowend);
+            const int32_t wp = (int32_t)(wla & 0x3FFFFu);
+            const bool sv = (wlb & (kWalkOn << 16)) && wp < rowend && wp + 3 > rowend;
+            if (__any(sv)) {
+                if (sv) {
+                    const uint32_t a6 = (r0 ^ (16u * 7u)) + 14u;
+                    uint32_t v6, v7;
+                    asm volatile("ds_read_u8 %0, %2\n\tds_read_u8 %1, %2 offset:1\n\ts_waitcnt lgkmcnt(0)"
+                                 : "=&v"(v6), "=&v"(v7)
+                                 : "v"(a6)
+                                 : "memory");
+                    wlb = (wlb & 0xFFFF0000u) | v6 | (v7 << 8);
+                }
+            }
+        };
+
         // ---- stash (wave-uniform counters) ---------------------------------
         uint32_t st_head = 0, st_tail = 0, head_slot = 0, tail_slot = 0;
         uint32_t hpos = 0, tpos = 0, r_head = 0, r_tail = 0, hk = 0, hinfo = 0, tcs = 0, thdr = 0;
@@ -615,6 +738,16 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             for (int w = 0; w < 32; ++w) sout[w] = start ? F[w] : sout[w];
             sout[0] ^= start && b < 128u ? c0 : 0u;
         };
+        // WALK, around each boundary() call: datagram k ends at row byte
+        // b - 1 -- the rest of its walk (its bytes are intact until boundary()
+        // masks b's piece), its count; then the next one starts at b (an empty
+        // one ended there too: same start and header byte; at b = 128 it
+        // opens with the next row)
+        auto walk_end = [&](uint32_t t, bool ev, uint32_t b) {
+            const int32_t end = (int32_t)((t << 7) + b);
+            walk_fields(t, ev, end - 4, end);
+            if (ev) walk_close((uint32_t)(end - cs));
+        };
 
         // ---- rows ---------------------------------------------------------
         // Row step: sout = A sin ^ row, then every datagram boundary in the
@@ -627,6 +760,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             // are younger; the last row waits for everything, so no row load
             // is in flight once the loop ends (the compiler does not see them
             // and would hand their registers to the epilogue)
+            // WALK: the open container's entries in row t - 1, whose image the
+            // transpose below overwrites (the last row's are left to the
+            // global-memory finish after the loop)
+            if constexpr (WALK)
+                if (t > 0u) row_walk(t - 1u);
             if (t + 1u < R)
                 asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             else
@@ -663,7 +801,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 #pragma unroll
                 for (int p = 0; p < 8; ++p) rad[p] = rr ^ (16u * p);
                 read_row_pre(rad, rr ^ (16u * ((b >> 4) & 7u)), x, pre);
-                if (hdr_next) chdr = x[0] & 0xFFu;  // a datagram that started at this row's byte 0
+                if (hdr_next) {  // a datagram that started at this row's byte 0
+                    chdr = x[0] & 0xFFu;
+                    if constexpr (WALK) walk_open();
+                }
                 hdr_next = false;
                 lnl_net_row_x(sin, x, sout);
             }
@@ -674,7 +815,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             // more boundaries in one lane loop below)
             {
                 const bool take = ev && cs >= -(int32_t)Sb;  // (a row's first boundary never ends an empty datagram)
+                if constexpr (WALK) walk_end(t, ev, b);
                 boundary(t, ev, false, b, take, sout, &pre);
+                if constexpr (WALK)
+                    if (ev && b < 128u) walk_open();
             }
             refill();
             ev = is_open() && Q.front() <= rowend;
@@ -682,7 +826,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint32_t b = ev ? Q.front() - rowst : 128u;
                 const bool zero = ev && cs == (int32_t)(rowst + b);  // empty datagram (CRC written by the pre-pass)
                 const bool take = ev && !zero;                     // (started in this row: never a head)
+                if constexpr (WALK) walk_end(t, ev, b);
                 boundary(t, ev, zero, b, take, sout, nullptr);
+                if constexpr (WALK)
+                    if (ev && b < 128u) walk_open();
                 refill();
                 ev = is_open() && Q.front() <= rowend;
             }
@@ -703,6 +850,32 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         }
 
         LNL_TL(3);
+        if constexpr (WALK) {
+            // an owned datagram still open runs on into the next segment(s):
+            // finish its walk from global memory
+            if (wlb & (kWalkOwned << 16)) {
+                const uint64_t ds = segbase + (uint64_t)(int64_t)cs;
+                const int64_t size = (int64_t)(bsh + A.off[k + 1u] - ds) - 4;
+                if (!(wlb & (kWalkMerged << 16))) {
+                    A.wrec[k] = (uint32_t)size;
+                    A.wcnt[k] = 1u;
+                } else {
+                    int64_t pos = (int64_t)(int32_t)(wla & 0x3FFFFu) - cs;
+                    uint32_t c = wla >> 18;
+                    while ((wlb & (kWalkOn << 16)) && pos + 2 <= size) {
+                        const uint32_t v = global_load3(ds + (uint64_t)pos);
+                        const int64_t L = (int64_t)(v & 0xFFFFu);
+                        pos += 2;
+                        if (L > size - pos || L == 0 || !lnl_packet_verify_hdr((uint8_t)(v >> 16), (uint64_t)L)) break;
+                        if (c < kDispatchRec) A.wrec[(size_t)c * n + k] = ((uint32_t)pos << 16) | (uint32_t)L;
+                        ++c;
+                        pos += L;
+                    }
+                    A.wcnt[k] = c;
+                }
+                wlb = 0u;
+            }
+        }
         // ---- the tail: the datagram still open, if it started here and ends
         // in the next segment; then fold everything still waiting -----------
         refill();
@@ -789,7 +962,10 @@ hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {
     const uint32_t blocks = (a.n + 255u) / 256u;
     const uint32_t prep = blocks < 8192u ? blocks : 8192u;
     hipLaunchKernelGGL(span_prep_kernel, dim3(prep), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(crc32c_span_kernel, dim3(grid), dim3(kThreads), 0, stream, a);
+    if (a.wcnt)
+        hipLaunchKernelGGL(crc32c_span_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
+    else
+        hipLaunchKernelGGL(crc32c_span_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a);
     return hipGetLastError();
 }
 

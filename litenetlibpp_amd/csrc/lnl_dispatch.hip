@@ -106,6 +106,29 @@ __global__ __launch_bounds__(256) void dispatch_count_kernel(DispatchArgs a) {
     a.counts[i] = c;
 }
 
+// Pass 1 of the fused path: the span kernel has walked every datagram whose
+// first byte it streamed (counts, rec); keep the counts of accepted datagrams,
+// zero the rest, and walk the few it left kWalkPending (e.g. a batch the span
+// kernel did not take).
+__global__ __launch_bounds__(256) void dispatch_fix_kernel(DispatchArgs a) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= a.n) return;
+    const uint8_t st = a.status[i];
+    uint32_t c = a.counts[i];
+    if (st != 1u) {
+        c = 0;
+    } else if (c == kWalkPending) {
+        const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
+        const uint32_t size = (uint32_t)(o1 - o0) - 4u;
+        uint32_t k = 0;
+        c = walk(a, o0 - a.off0, size, [&](uint32_t pos, uint32_t len) {
+            if (k < kDispatchRec) a.rec[(size_t)k * a.n + i] = (pos << 16) | len;
+            ++k;
+        });
+    }
+    a.counts[i] = c;
+}
+
 // Pass 2: datagram i's packets go to [first[i], first[i] + counts[i]).  A
 // wave owns 64 consecutive datagrams, whose packets form one contiguous range
 // of the output.  Datagrams whose packets all sit in pass 1's records (at most
@@ -355,6 +378,17 @@ hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_by
     if (a.look) return hipErrorInvalidValue;  // the one-pass form is not in the product build
 #endif
     hipLaunchKernelGGL(dispatch_count_kernel, grid, dim3(256), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, a.counts, a.first, (int)a.n, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(dispatch_emit_kernel, grid, dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dispatch_walked(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream) {
+    const dim3 grid((a.n + 255u) / 256u);
+    hipLaunchKernelGGL(dispatch_fix_kernel, grid, dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, a.counts, a.first, (int)a.n, stream);

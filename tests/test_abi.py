@@ -37,7 +37,7 @@ def test_header_declares_the_boundary():
               "lnl_crc32c_layer_outbound", "lnl_crc32c_layer_inbound", "lnl_crc32c_last_error",
               "lnl_crc32c_batch_host_multi", "lnl_packet_verify", "lnl_inbound_status",
               "lnl_inbound_filter_csr_dev", "lnl_inbound_filter_host", "lnl_ingress_recv_batch",
-              "lnl_dispatch_csr_dev", "lnl_xor_layer", "lnl_xor_layer_csr_dev", "lnl_xor_layer_fixed_dev"):
+              "lnl_dispatch_csr_dev", "lnl_inbound_filter_dispatch_csr_dev", "lnl_xor_layer", "lnl_xor_layer_csr_dev", "lnl_xor_layer_fixed_dev"):
         assert s in syms
 
 
@@ -47,7 +47,23 @@ def test_library_exports_every_declared_symbol(pkg):
     exported = set(re.findall(r"\bT (lnl_\w+)", out))
     missing = [s for s in declared_symbols() if s not in exported]
     assert not missing, missing
-    assert pkg.lib().lnl_crc32c_abi_version() == 6
+    assert pkg.lib().lnl_crc32c_abi_version() == 7
+
+
+def test_ctypes_bindings_match_the_header(pkg):
+    """Every entry point the Python mirror binds takes as many arguments as
+    include/lnl_crc32c.h declares."""
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    L = pkg.lib()
+    checked = 0
+    for name, params in re.findall(r"\b(lnl_\w+)\s*\(([^)]*)\)\s*;", txt):
+        argtypes = getattr(getattr(L, name), "argtypes", None)
+        if argtypes is None:
+            continue
+        count = 0 if params.strip() in ("", "void") else params.count(",") + 1
+        assert len(argtypes) == count, (name, len(argtypes), count)
+        checked += 1
+    assert checked >= 15
 
 
 def test_cpu_crc_matches_oracle(pkg):

@@ -584,6 +584,92 @@ def test_dispatch_records_and_rewalk(P):
     assert got == exp and len(exp) == 50 * (3 + 8 + 9 + 400 + 1)
 
 
+def _packets(off, start, length, parent):
+    par = parent.cpu().numpy()
+    return list(zip(par.tolist(), (start.cpu().numpy() - off[par].astype(np.int64)).tolist(),
+                    length.cpu().numpy().tolist()))
+
+
+def _fused_vs_two_calls(P, wires, cap_check=True):
+    """lnl_inbound_filter_dispatch_csr_dev against lnl_inbound_filter_csr_dev +
+    lnl_dispatch_csr_dev and against oracle.inbound_status / oracle.dispatch."""
+    off = np.concatenate([[0], np.cumsum([len(w) for w in wires])]).astype(np.uint64)
+    # bytes after the batch that read as a MERGED container: nothing may walk them
+    trail = bytes([0x0C]) + b"".join(bytes([1, 0, 0]) for _ in range(40))
+    blob = np.frombuffer(b"".join(wires) + trail, np.uint8)
+    d, o = dev(blob), dev(off.view(np.int64), torch.int64)
+    status, start, length, parent = P.filter_dispatch(d, o)
+    st2 = P.inbound_filter(d, o)
+    s2, l2, p2 = P.dispatch(d, o, st2)
+    st = status.cpu().numpy()
+    assert np.array_equal(st, st2.cpu().numpy())
+    exp_st = np.array([oracle.inbound_status(np.frombuffer(w, np.uint8)) for w in wires], np.uint8)
+    bad = np.nonzero(st != exp_st)[0]
+    assert bad.size == 0, f"{bad.size} status mismatches, first at {bad[:5]}"
+    got = _packets(off, start, length, parent)
+    assert got == _packets(off, s2, l2, p2)
+    exp = oracle.dispatch([np.frombuffer(w, np.uint8) for w in wires], st)
+    assert got == exp
+    if cap_check:
+        _, _, _, p3 = P.filter_dispatch(d, o, cap=11)
+        assert p3.cpu().numpy().tolist() == [e[0] for e in exp[:11]]
+    return exp
+
+
+@pytest.mark.parametrize("n", [20000, 120000])
+def test_filter_dispatch_fused(P, n):
+    """Filter + dispatch in one pass (the span kernel walks each MERGED
+    container while its bytes are in LDS): same statuses and packets as the two
+    calls, and as the oracle, for well-formed, truncated, rejected-entry,
+    zero-length-entry and nested containers, plain datagrams, runts and
+    corrupted CRCs; containers long enough to cross segments (and, at n =
+    20000, three or more of them: 2 KiB segments) and entries that straddle rows."""
+    rng = np.random.default_rng(4242 + n)
+    layer = P.Crc32cLayer()
+    wires = []
+    for i in range(n):
+        r = rng.random()
+        if r < 0.55:
+            big = rng.random() < 0.1
+            parts = [bytes([int(rng.choice([0x00, 0x01, 0x03]))]) +
+                     rng.integers(0, 256, int(rng.integers(3, 700 if big else 60)), dtype=np.uint8).tobytes()
+                     for _ in range(int(rng.integers(0, 12)))]
+            mode = rng.choice(["ok", "ok", "ok", "truncated", "bad_sub", "zero_len"])
+            body = _merged(rng, parts, mode)
+            if rng.random() < 0.05:
+                body = _merged(rng, [body], "ok")
+        elif r < 0.6:
+            body = bytes(int(rng.integers(0, 4)))                                   # runts
+        else:
+            body = bytes([int(rng.choice([0x00, 0x01, 0x1F, 0x8C]))]) + \
+                rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8).tobytes()
+        w = bytearray(layer.process_outbound(body))
+        if rng.random() < 0.03:
+            w[int(rng.integers(0, len(w)))] ^= 0x04
+        wires.append(bytes(w))
+    exp = _fused_vs_two_calls(P, wires)
+    assert sum(1 for (_, pos, _) in exp if pos > 0) > n // 10
+
+
+def test_filter_dispatch_fused_shapes(P):
+    """Fused path, container shapes at the walk's edges: > 8 entries (emit
+    walks again), datagrams >= 64 KiB (16-bit records), many 1..3-byte
+    entries (several per row, entries straddling rows), and the bench's 5 x
+    256-B shape, in a batch large enough for the span path."""
+    rng = np.random.default_rng(99)
+    layer = P.Crc32cLayer()
+    sub = lambda m: bytes([0x00]) + rng.integers(0, 256, m - 1, dtype=np.uint8).tobytes()
+    bodies = [_merged(rng, [sub(30000) for _ in range(3)], "ok"),
+              _merged(rng, [sub(20) for _ in range(9)], "ok"),
+              _merged(rng, [sub(int(rng.integers(1, 4))) for _ in range(500)], "ok"),
+              bytes([0x01]) + sub(70000)]
+    wires = [bytes(layer.process_outbound(b)) for b in bodies] * 12
+    wires += [bytes(layer.process_outbound(_merged(rng, [sub(256) for _ in range(5)], "ok")))
+              for _ in range(20000)]
+    order = rng.permutation(len(wires))
+    _fused_vs_two_calls(P, [wires[i] for i in order])
+
+
 @pytest.mark.parametrize("klen", [1, 3, 16, 37, 256])
 def test_xor_layer_csr(P, klen):
     """XorEncryptLayer over a device CSR batch, in place: every datagram equals
