@@ -190,7 +190,8 @@ struct SpanArgs {
     uint8_t* thdr;
     // filter + dispatch (kSpanFilter only; null otherwise): the MERGED walk of
     // every datagram, done by the lane its first byte streams through --
-    // DispatchArgs::counts / rec layout; kWalkPending where no lane walked it
+    // DispatchArgs::counts / rec layout; kWalkPending where no lane walked
+    // it, kWalkPlain for a datagram that is not a container
     uint32_t* wcnt;
     uint32_t* wrec;
 };
@@ -291,6 +292,7 @@ struct DispatchArgs {
 };
 constexpr uint32_t kDispatchRec = 8;  // packets per datagram kept from the counting walk
 constexpr uint32_t kWalkPending = 0xFFFFFFFFu;  // counts[i]: not walked yet (fused path)
+constexpr uint32_t kWalkPlain = 0x80000000u;    // counts[i]: not a container, one packet (fused path)
 size_t dispatch_scan_bytes(uint32_t n);
 hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
 // Fused path (lnl_inbound_filter_dispatch_csr_dev): counts / rec already hold

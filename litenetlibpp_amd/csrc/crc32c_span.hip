@@ -306,6 +306,15 @@ __device__ LNL_INLINE uint32_t global_load3(uint64_t q) {
 }
 
 constexpr uint32_t kMergedProperty = 12;  // PACKET_PROPERTY::MERGED, net_enums.h:60
+
+// lnl_packet_verify_hdr (lnl_packet.h) for a packet of size < 2^16 whose first
+// byte is b0 & 0xFF, in 32-bit arithmetic
+__device__ LNL_INLINE bool verify_hdr16(uint32_t b0, uint32_t size) {
+    const uint32_t p = b0 & 0x1Fu;
+    const uint32_t hs = lnl_packet_header_size(p < LNL_PACKET_PROPERTY_COUNT ? p : 0u);
+    const uint32_t need = (b0 & 0x80u) ? hs + LNL_FRAGMENT_HEADER_SIZE : hs;
+    return p < LNL_PACKET_PROPERTY_COUNT && size >= need;
+}
 // walk flags (WALK): the open datagram started in this lane's segment (the
 // lane writes its packet count), is a MERGED container, is still being walked
 enum : uint32_t { kWalkOwned = 1, kWalkMerged = 2, kWalkOn = 4 };
@@ -501,6 +510,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             }
         };
 
+
         // ---- MERGED walk (WALK only) ---------------------------------------
         // Two registers (the kernel is at the VGPR budget):
         //   wla = wp | wc << 18: wp, the next entry's u16 size field, bytes from
@@ -508,7 +518,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         //        taken (< Sb / 3 < 2^14)
         //   wlb = wsv | wfl << 16: wsv, bytes 126, 127 of the previous row; wfl,
         //        the walk flags
-        uint32_t wla = 0u, wlb = 0u;
+        uint32_t wla = 0u, wlb = 0u, wsv_next = 0u;
         // bytes q, q + 1, q + 2 (q >= the row's first byte - 2) of row t
         auto walk_read3 = [&](uint32_t t, int32_t q) -> uint32_t {
             const int32_t j = q - (int32_t)(t << 7);
@@ -535,28 +545,30 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // before lim; size_end: the container's end without the CRC field
         // (the walk rules of lnl_dispatch.hip walk(), segment-relative)
         auto walk_fields = [&](uint32_t t, bool sel, int32_t size_end, int32_t lim) {
-            bool act = sel && (wlb & (kWalkOn << 16));
+            // a lane has work while walking and its next entry either ends the
+            // walk (past the container) or has its three bytes before lim
+            auto due = [&]() {
+                const int32_t wp = (int32_t)(wla & 0x3FFFFu);
+                return sel && (wlb & (kWalkOn << 16)) && (wp + 2 > size_end || wp + 3 <= lim);
+            };
+            bool act = due();
             while (__any(act)) {
                 if (act) {
                     const int32_t wp = (int32_t)(wla & 0x3FFFFu);
                     const uint32_t wc = wla >> 18;
-                    if (wp + 2 > size_end) {
-                        wlb &= ~(kWalkOn << 16);
-                        act = false;
-                    } else if (wp + 3 > lim) {
-                        act = false;  // next row
-                    } else {
+                    bool stop = wp + 2 > size_end;
+                    if (!stop) {
                         const uint32_t v = walk_read3(t, wp);
                         const int32_t L = (int32_t)(v & 0xFFFFu), p2 = wp + 2;
-                        if (L > size_end - p2 || L == 0 || !lnl_packet_verify_hdr((uint8_t)(v >> 16), (uint32_t)L)) {
-                            wlb &= ~(kWalkOn << 16);
-                            act = false;
-                        } else {
-                            if (wc < kDispatchRec) A.wrec[(size_t)wc * n + k] = ((uint32_t)(p2 - cs) << 16) | (uint32_t)L;
+                        stop = L > size_end - p2 || L == 0 || !verify_hdr16(v >> 16, (uint32_t)L);
+                        if (!stop) {
+                            if (wc < kDispatchRec) A.wrec[wc * n + k] = ((uint32_t)(p2 - cs) << 16) | (uint32_t)L;
                             wla = (uint32_t)(p2 + L) | ((wc + 1u) << 18);
                         }
                     }
+                    if (stop) wlb &= ~(kWalkOn << 16);
                 }
+                act = due();
             }
         };
         // datagram k (owned) starts at cs with header byte chdr (k = n: the
@@ -568,37 +580,21 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // datagram k ends, len bytes: its packet count (a plain one is one
         // packet, the whole datagram without the CRC field)
         auto walk_close = [&](uint32_t len) {
-            if (wlb & (kWalkOwned << 16)) {
-                if (wlb & (kWalkMerged << 16)) {
-                    A.wcnt[k] = wla >> 18;
-                } else {
-                    A.wrec[k] = len - 4u;
-                    A.wcnt[k] = 1u;
-                }
-            }
+            if (wlb & (kWalkOwned << 16))  // (a plain datagram's record is the fix-up's: its length)
+                A.wcnt[k] = (wlb & (kWalkMerged << 16)) ? wla >> 18 : kWalkPlain;
             wlb = 0u;
         };
-        // once row t's boundaries are done (called before row t + 1's
-        // transpose): the open container's entries in row t, and the row's
-        // last two bytes when an entry straddles into row t + 1
+        // after row t's boundaries: the open container's entries in row t (an
+        // entry that straddles into row t + 1 reads the row's last two bytes
+        // from wsv in the next row)
         auto row_walk = [&](uint32_t t) {
+#if defined(LNL_WALK_DIAG) && (LNL_WALK_DIAG & 1)
+            return;  // diagnostic build only (wrong packets)
+#endif
             const int32_t rowend = (int32_t)(t << 7) + 128;
             // (a boundary clamped to 0xFFFF lies beyond the segment: no bound yet)
             const uint32_t qf = Q.front();
             walk_fields(t, true, qf == 0xFFFFu ? 0x7FFFFFFF : (int32_t)qf - 4, rowend);
-            const int32_t wp = (int32_t)(wla & 0x3FFFFu);
-            const bool sv = (wlb & (kWalkOn << 16)) && wp < rowend && wp + 3 > rowend;
-            if (__any(sv)) {
-                if (sv) {
-                    const uint32_t a6 = (r0 ^ (16u * 7u)) + 14u;
-                    uint32_t v6, v7;
-                    asm volatile("ds_read_u8 %0, %2\n\tds_read_u8 %1, %2 offset:1\n\ts_waitcnt lgkmcnt(0)"
-                                 : "=&v"(v6), "=&v"(v7)
-                                 : "v"(a6)
-                                 : "memory");
-                    wlb = (wlb & 0xFFFF0000u) | v6 | (v7 << 8);
-                }
-            }
         };
 
         // ---- stash (wave-uniform counters) ---------------------------------
@@ -744,6 +740,9 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // one ended there too: same start and header byte; at b = 128 it
         // opens with the next row)
         auto walk_end = [&](uint32_t t, bool ev, uint32_t b) {
+#if defined(LNL_WALK_DIAG) && (LNL_WALK_DIAG & 2)
+            return;  // diagnostic build only (wrong packets)
+#endif
             const int32_t end = (int32_t)((t << 7) + b);
             walk_fields(t, ev, end - 4, end);
             if (ev) walk_close((uint32_t)(end - cs));
@@ -760,11 +759,17 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             // are younger; the last row waits for everything, so no row load
             // is in flight once the loop ends (the compiler does not see them
             // and would hand their registers to the epilogue)
-            // WALK: the open container's entries in row t - 1, whose image the
-            // transpose below overwrites (the last row's are left to the
-            // global-memory finish after the loop)
+            // WALK: the open container's entries in row t - 1 (its image is
+            // still there until the transpose below; the last row's are left
+            // to the global-memory finish after the loop), while row t's loads
+            // land; the straddling entry's bytes 126, 127 of row t - 1 come
+            // from wsv_next (taken from the row's registers as it streamed)
+            // (measured the same after the wait)
             if constexpr (WALK)
-                if (t > 0u) row_walk(t - 1u);
+                if (t > 0u) {
+                    row_walk(t - 1u);
+                    wlb = (wlb & 0xFFFF0000u) | wsv_next;
+                }
             if (t + 1u < R)
                 asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             else
@@ -806,6 +811,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     if constexpr (WALK) walk_open();
                 }
                 hdr_next = false;
+                if constexpr (WALK) wsv_next = x[31] >> 16;  // bytes 126, 127
                 lnl_net_row_x(sin, x, sout);
             }
             sout[0] ^= inj;
@@ -857,11 +863,13 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint64_t ds = segbase + (uint64_t)(int64_t)cs;
                 const int64_t size = (int64_t)(bsh + A.off[k + 1u] - ds) - 4;
                 if (!(wlb & (kWalkMerged << 16))) {
-                    A.wrec[k] = (uint32_t)size;
-                    A.wcnt[k] = 1u;
+                    A.wcnt[k] = kWalkPlain;
                 } else {
                     int64_t pos = (int64_t)(int32_t)(wla & 0x3FFFFu) - cs;
                     uint32_t c = wla >> 18;
+#if defined(LNL_WALK_DIAG) && (LNL_WALK_DIAG & 4)
+                    wlb = 0u;  // diagnostic build only (wrong packets)
+#endif
                     while ((wlb & (kWalkOn << 16)) && pos + 2 <= size) {
                         const uint32_t v = global_load3(ds + (uint64_t)pos);
                         const int64_t L = (int64_t)(v & 0xFFFFu);

@@ -117,6 +117,9 @@ __global__ __launch_bounds__(256) void dispatch_fix_kernel(DispatchArgs a) {
     uint32_t c = a.counts[i];
     if (st != 1u) {
         c = 0;
+    } else if (c == kWalkPlain) {  // the datagram itself, CRC stripped
+        a.rec[i] = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
+        c = 1;
     } else if (c == kWalkPending) {
         const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
         const uint32_t size = (uint32_t)(o1 - o0) - 4u;

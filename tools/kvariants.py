@@ -32,6 +32,10 @@ VARIANTS = {
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
     "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
     "app_t64": "-DLNL_APPEND_TEAM=64",              # append kernel: 64 lanes per datagram (default 32)
+    "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)
+    "walk_noend": "-DLNL_WALK_DIAG=2",              # ... no walk at datagram ends (wrong packets)
+    "walk_notail": "-DLNL_WALK_DIAG=4",             # ... no global-memory finish (wrong packets)
+    "walk_none": "-DLNL_WALK_DIAG=7",               # ... none of the three (wrong packets)
     "span_noflush": "-DLNL_SPAN_DIAG=4",            # CSR span kernel: stash entries dropped unread (wrong CRCs)
     "span_noput": "-DLNL_SPAN_DIAG=12",             # ... and not written either (wrong CRCs)
     "bucketed": ("", 4),                            # CSR: the bucketed batch kernel (previous default)
@@ -173,6 +177,32 @@ def run(names, rounds, workloads):
             def call(L):
                 L.lnl_crc32c_append_csr_dev(data.data_ptr(), off.data_ptr(), n_pk, wire.data_ptr(), out.data_ptr(),
                                             s.cuda_stream)
+        elif wl[0] == "fd":  # ("fd", n): filter + dispatch over n MERGED containers of 5 x 256-B packets
+            n_pk = wl[1]
+            S = 1 + 5 * 259 + 4
+            data = torch.randint(0, 256, (n_pk * S,), dtype=torch.uint8, device=dev, generator=g)
+            d2 = data.view(n_pk, S)
+            d2[:, 0] = 0x0C
+            for j in range(5):
+                d2[:, 1 + 259 * j] = 1
+                d2[:, 2 + 259 * j] = 1
+                d2[:, 3 + 259 * j] = 0
+            off = torch.arange(0, (n_pk + 1) * S, S, dtype=torch.int64, device=dev)
+            st = torch.empty(n_pk, dtype=torch.uint8, device=dev)
+            k = 5 * n_pk
+            pst = torch.empty(k, dtype=torch.int64, device=dev)
+            pl = torch.empty(k, dtype=torch.int32, device=dev)
+            pp = torch.empty(k, dtype=torch.int32, device=dev)
+            tot = torch.zeros(1, dtype=torch.int32, device=dev)
+            algo = n_pk * S + 8 * (n_pk + 1) + n_pk + 16 * k
+            wkey = f"fd{n_pk}"
+
+            def call(L):  # (CRC fields are random: statuses DROP, the walk still runs)
+                L.lnl_inbound_filter_dispatch_csr_dev(
+                    ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), ctypes.c_uint32(n_pk),
+                    ctypes.c_void_p(st.data_ptr()), ctypes.c_void_p(pst.data_ptr()), ctypes.c_void_p(pl.data_ptr()),
+                    ctypes.c_void_p(pp.data_ptr()), ctypes.c_uint32(k), ctypes.c_void_p(tot.data_ptr()),
+                    ctypes.c_void_p(s.cuda_stream))
         else:
             n_pk, L_pk, stride, shift = wl
             buf = torch.randint(0, 256, (n_pk * stride + 256,), dtype=torch.uint8, device=dev, generator=g)
@@ -217,7 +247,7 @@ def main():
     if a.cmd == "build":
         build(names)
     else:
-        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.split(":")[0] in ("csr", "xor", "append", "filter")
+        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.split(":")[0] in ("csr", "xor", "append", "filter", "fd")
               else tuple(int(v) for v in w.split(":")) for w in a.workloads.split(",")]
         res = run(names, a.rounds, wl)
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
