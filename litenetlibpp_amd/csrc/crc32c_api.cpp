@@ -150,10 +150,11 @@ int grid_for_waves(const DeviceState& S, uint32_t waves, int threads = lnl::kBlo
     return (int)std::max(1u, std::min(wgs, cap));
 }
 
-int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
+int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st, uint32_t max_wgs = 0xFFFFFFFFu) {
     a.dummy = S.dummy;
     a.fold = S.fold;
-    hipError_t e = lnl::launch_crc32c_batch(a, mode, grid_for_waves(S, (a.n + 63u) / 64u), st);
+    const int grid = std::min(grid_for_waves(S, (a.n + 63u) / 64u), (int)std::min(max_wgs, 0x7FFFFFFFu));
+    hipError_t e = lnl::launch_crc32c_batch(a, mode, std::max(grid, 1), st);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     return 0;
 }
@@ -318,6 +319,9 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 }
 #endif  // LNL_EXPERIMENTS
 
+#ifndef LNL_SPAN_FIX_WGS
+#define LNL_SPAN_FIX_WGS 0xFFFFFFFFu  // cap on the batch kernel's grid after the span kernel (experiments)
+#endif
 // CSR batches (product path): the span kernel (crc32c_span.hip: every line read
 // once, one 512-thread workgroup per CU) after its pre-pass, then the batch
 // kernel, which completes the cross-segment heads and takes the datagrams the
@@ -354,7 +358,7 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
         o.span_ctl = g.ctl;
         o.span_tab = S.span_tab;
         o.span_thdr = g.thdr;
-        rc = launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st);
+        rc = launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st, LNL_SPAN_FIX_WGS);
     }
     e = hipFreeAsync(scratch, st);
     if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
@@ -828,7 +832,7 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     }
     const size_t scan_bytes = lnl::dispatch_scan_bytes(n);
     void* scratch = nullptr;
-    const size_t bytes = (2 + (size_t)lnl::kDispatchRec) * n * 4 + scan_bytes + 256;
+    const size_t bytes = (3 + (size_t)lnl::kDispatchRec) * n * 4 + scan_bytes + 256;  // + the walk's spare record slot
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
     if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
     lnl::DispatchArgs a{};
@@ -844,7 +848,7 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     a.pkt_parent = d_pkt_parent;
     a.cap = cap;
     a.total = d_total;
-    void* tmp = (void*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);
+    void* tmp = (void*)(((uintptr_t)(a.rec + (size_t)(lnl::kDispatchRec + 1) * n) + 255) & ~(uintptr_t)255);
     lnl::BatchArgs b{};
     b.base = d_base;
     b.off = d_off;

@@ -190,8 +190,9 @@ struct SpanArgs {
     uint8_t* thdr;
     // filter + dispatch (kSpanFilter only; null otherwise): the MERGED walk of
     // every datagram, done by the lane its first byte streams through --
-    // DispatchArgs::counts / rec layout; kWalkPending where no lane walked
-    // it, kWalkPlain for a datagram that is not a container
+    // DispatchArgs::counts / rec layout plus a spare record slot kDispatchRec;
+    // kWalkPending where no lane walked it, kWalkPlain for a datagram that is
+    // not a container
     uint32_t* wcnt;
     uint32_t* wrec;
 };

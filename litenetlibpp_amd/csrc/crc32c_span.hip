@@ -61,6 +61,9 @@ constexpr uint32_t kEntry = 144;   // stash entry stride: 128 B of state + 16 B 
                                    // consecutive slots start on different banks and the 8
                                    // pieces of an entry sit at immediate offsets
 constexpr uint32_t kImageBytes = 8192;
+#ifndef LNL_SPAN_PREP_BLOCKS
+#define LNL_SPAN_PREP_BLOCKS 8192u  // pre-pass grid cap (256-thread workgroups, grid-stride)
+#endif
 #ifndef LNL_SPAN_PRIO
 #define LNL_SPAN_PRIO 0  // 0: progress-based issue priority; 1: static (experiment); 2: none
 #endif
@@ -553,20 +556,18 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             };
             bool act = due();
             while (__any(act)) {
-                if (act) {
+                if (act) {  // one entry, branch-free: the read is harmless when the walk stops here
                     const int32_t wp = (int32_t)(wla & 0x3FFFFu);
                     const uint32_t wc = wla >> 18;
-                    bool stop = wp + 2 > size_end;
-                    if (!stop) {
-                        const uint32_t v = walk_read3(t, wp);
-                        const int32_t L = (int32_t)(v & 0xFFFFu), p2 = wp + 2;
-                        stop = L > size_end - p2 || L == 0 || !verify_hdr16(v >> 16, (uint32_t)L);
-                        if (!stop) {
-                            if (wc < kDispatchRec) A.wrec[wc * n + k] = ((uint32_t)(p2 - cs) << 16) | (uint32_t)L;
-                            wla = (uint32_t)(p2 + L) | ((wc + 1u) << 18);
-                        }
-                    }
-                    if (stop) wlb &= ~(kWalkOn << 16);
+                    const bool in = wp + 2 <= size_end;
+                    const uint32_t v = walk_read3(t, in ? wp : (int32_t)(t << 7));
+                    const int32_t L = (int32_t)(v & 0xFFFFu), p2 = wp + 2;
+                    const bool ok = in && L != 0 && L <= size_end - p2 && verify_hdr16(v >> 16, (uint32_t)L);
+                    // record slot wc (slot kDispatchRec is a spare the emit pass never
+                    // reads; a slot written as the walk stops is past its count)
+                    A.wrec[(wc < kDispatchRec ? wc : kDispatchRec) * n + k] = ((uint32_t)(p2 - cs) << 16) | (uint32_t)L;
+                    wla = ok ? ((uint32_t)(p2 + L) | ((wc + 1u) << 18)) : wla;
+                    wlb = ok ? wlb : (wlb & ~(kWalkOn << 16));
                 }
                 act = due();
             }
@@ -968,7 +969,7 @@ void span_scratch_layout(SpanArgs& a, uint32_t* s) {
 
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {
     const uint32_t blocks = (a.n + 255u) / 256u;
-    const uint32_t prep = blocks < 8192u ? blocks : 8192u;
+    const uint32_t prep = blocks < LNL_SPAN_PREP_BLOCKS ? blocks : LNL_SPAN_PREP_BLOCKS;
     hipLaunchKernelGGL(span_prep_kernel, dim3(prep), dim3(256), 0, stream, a);
     if (a.wcnt)
         hipLaunchKernelGGL(crc32c_span_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
