@@ -62,7 +62,7 @@ constexpr uint32_t kEntry = 144;   // stash entry stride: 128 B of state + 16 B 
                                    // pieces of an entry sit at immediate offsets
 constexpr uint32_t kImageBytes = 8192;
 #ifndef LNL_SPAN_PREP_BLOCKS
-#define LNL_SPAN_PREP_BLOCKS 8192u  // pre-pass grid cap (256-thread workgroups, grid-stride)
+#define LNL_SPAN_PREP_BLOCKS 1024u  // pre-pass grid cap (256-thread workgroups, grid-stride; 1024 measured 1 % faster than 8192, 256 slower)
 #endif
 #ifndef LNL_SPAN_PRIO
 #define LNL_SPAN_PRIO 0  // 0: progress-based issue priority; 1: static (experiment); 2: none

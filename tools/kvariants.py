@@ -32,10 +32,9 @@ VARIANTS = {
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
     "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
     "app_t64": "-DLNL_APPEND_TEAM=64",              # append kernel: 64 lanes per datagram (default 32)
-    "prep1k": "-DLNL_SPAN_PREP_BLOCKS=1024u",       # span pre-pass: 1024 workgroups (4 per CU), grid-stride
+    "prep8k": "-DLNL_SPAN_PREP_BLOCKS=8192u",       # span pre-pass: 8192 workgroups (before: 1 % slower than 1024)
     "prep256": "-DLNL_SPAN_PREP_BLOCKS=256u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
-    "prep1k_fix64": "-DLNL_SPAN_PREP_BLOCKS=1024u -DLNL_SPAN_FIX_WGS=64u",
     "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)
     "walk_noend": "-DLNL_WALK_DIAG=2",              # ... no walk at datagram ends (wrong packets)
     "walk_notail": "-DLNL_WALK_DIAG=4",             # ... no global-memory finish (wrong packets)
