@@ -329,11 +329,10 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 // (span_mode: kSpanCrc -> out[i]; kSpanVerify / kSpanFilter -> ok[i], the
 // overflow datagrams through the batch kernel in verify mode)
 int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st, uint32_t span_mode = lnl::kSpanCrc,
-                    uint32_t* walk_counts = nullptr, uint32_t* walk_rec = nullptr) {
+                    uint32_t* walk_blocks = nullptr) {
     lnl::SpanArgs g{};
     g.mode = span_mode;
-    g.wcnt = walk_counts;  // filter + dispatch: the MERGED walk in the same pass
-    g.wrec = walk_rec;
+    g.wblk = walk_blocks;  // filter + dispatch: the MERGED walk in the same pass
     g.ok = a.ok;
     g.base = a.base;
     g.off = a.off;
@@ -832,7 +831,7 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     }
     const size_t scan_bytes = lnl::dispatch_scan_bytes(n);
     void* scratch = nullptr;
-    const size_t bytes = (3 + (size_t)lnl::kDispatchRec) * n * 4 + scan_bytes + 256;  // + the walk's spare record slot
+    const size_t bytes = (2 + (size_t)lnl::kDispatchRec + lnl::kWalkBlock) * n * 4 + scan_bytes + 512;
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
     if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
     lnl::DispatchArgs a{};
@@ -848,14 +847,17 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     a.pkt_parent = d_pkt_parent;
     a.cap = cap;
     a.total = d_total;
-    void* tmp = (void*)(((uintptr_t)(a.rec + (size_t)(lnl::kDispatchRec + 1) * n) + 255) & ~(uintptr_t)255);
+    uint32_t* blk = (uint32_t*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);
+    a.blk = blk;
+    a.span_waves = (uint32_t)S->cus * (uint32_t)(lnl::kSpanThreads / 64);
+    void* tmp = (void*)(((uintptr_t)(blk + (size_t)lnl::kWalkBlock * n) + 255) & ~(uintptr_t)255);
     lnl::BatchArgs b{};
     b.base = d_base;
     b.off = d_off;
     b.n = n;
     b.ok = d_status;
     b.filter = 1u;
-    int rc = launch_csr_span(*S, b, st, lnl::kSpanFilter, a.counts, a.rec);
+    int rc = launch_csr_span(*S, b, st, lnl::kSpanFilter, blk);
     if (rc == 0 && (e = lnl::launch_dispatch_walked(a, tmp, scan_bytes, st)) != hipSuccess)
         rc = hip_fail(e, "dispatch launch");
     e = hipFreeAsync(scratch, st);

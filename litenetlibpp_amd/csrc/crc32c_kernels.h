@@ -189,12 +189,10 @@ struct SpanArgs {
     uint8_t* ok;
     uint8_t* thdr;
     // filter + dispatch (kSpanFilter only; null otherwise): the MERGED walk of
-    // every datagram, done by the lane its first byte streams through --
-    // DispatchArgs::counts / rec layout plus a spare record slot kDispatchRec;
-    // kWalkPending where no lane walked it, kWalkPlain for a datagram that is
-    // not a container
-    uint32_t* wcnt;
-    uint32_t* wrec;
+    // every datagram, done by the lane its first byte streams through, into
+    // one 8-word block per datagram: [count, record 0 .. 6] (kWalkPlain: not a
+    // container); dispatch_fix_kernel turns the blocks into counts + records
+    uint32_t* wblk;
 };
 size_t span_scratch_words(uint32_t n, uint32_t waves);
 void span_scratch_layout(SpanArgs& a, uint32_t* scratch);
@@ -290,15 +288,20 @@ struct DispatchArgs {
     uint32_t* pkt_parent;   // cap: datagram index
     uint32_t cap;
     uint32_t* total;        // device: packets delivered (may exceed cap)
+    // fused path (dispatch_fix_kernel): the span kernel's walk blocks, and the
+    // resident waves its geometry was computed for (to tell whether it ran)
+    const uint32_t* blk;
+    uint32_t span_waves;
 };
 constexpr uint32_t kDispatchRec = 8;  // packets per datagram kept from the counting walk
-constexpr uint32_t kWalkPending = 0xFFFFFFFFu;  // counts[i]: not walked yet (fused path)
-constexpr uint32_t kWalkPlain = 0x80000000u;    // counts[i]: not a container, one packet (fused path)
+constexpr uint32_t kWalkBlock = 8;             // fused path: words per datagram block [count, 7 records]
+constexpr uint32_t kWalkPlain = 0x80000000u;    // block count: not a container, one packet
 size_t dispatch_scan_bytes(uint32_t n);
 hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
-// Fused path (lnl_inbound_filter_dispatch_csr_dev): counts / rec already hold
-// the span kernel's walk; the fix-up zeroes the counts of datagrams not
-// accepted and walks the kWalkPending ones, then scan + emit as above.
+// Fused path (lnl_inbound_filter_dispatch_csr_dev): the fix-up turns the span
+// kernel's walk blocks into counts + records (zero for datagrams not
+// accepted; walking again only what the blocks cannot hold), then scan + emit
+// as above.
 hipError_t launch_dispatch_walked(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
 
 // Verify epilogue (crc32c_verify.hip): ok / body CRC from wire-datagram CRCs.

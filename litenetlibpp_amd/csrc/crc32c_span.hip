@@ -128,7 +128,6 @@ __global__ __launch_bounds__(256) void span_prep_kernel(SpanArgs a) {
     }
     const uint32_t stride = gridDim.x * 256u;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-        if (a.wcnt) a.wcnt[i] = kWalkPending;  // filter + dispatch: the kernel walks what it owns
         if (whole) {
             a.ovf[i] = i;
             continue;
@@ -544,6 +543,24 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             if (j < -1) v1 = (wlb >> 8) & 0xFFu;
             return v0 | (v1 << 8) | (v2 << 16);
         };
+        // The datagram's block [count, records 0 .. 6] (crc32c_kernels.h): words
+        // 0 .. 3 gather in the lane's 16-byte pad of stash slot `lane` (free:
+        // entries use 128 of their 144 bytes) and go out as one 16-byte store
+        // with the count; records 3 .. 6 are stored directly (a block per
+        // datagram: one sector, where 4-byte stores of the slot-major layout
+        // each cost a partly written sector -- 12x the record bytes, measured)
+        const uint32_t wpad = stash + lane * kEntry + 128u;
+        auto walk_record = [&](uint32_t j, uint32_t r) {
+            if (j < 3u)
+                asm volatile("ds_write_b32 %0, %1 offset:4" ::"v"(wpad + 4u * j), "v"(r) : "memory");
+            else if (j < kWalkBlock - 1u)
+                A.wblk[k * kWalkBlock + 1u + j] = r;
+        };
+        auto walk_block = [&](uint32_t count) {
+            asm volatile("ds_write_b32 %0, %1" ::"v"(wpad), "v"(count) : "memory");
+            const u32x4 v = lds_read_piece(wpad);
+            *reinterpret_cast<uint4*>(A.wblk + k * kWalkBlock) = make_uint4(v.x, v.y, v.z, v.w);
+        };
         // take the entries of the owned container (sel) whose three bytes lie
         // before lim; size_end: the container's end without the CRC field
         // (the walk rules of lnl_dispatch.hip walk(), segment-relative)
@@ -565,7 +582,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     const bool ok = in && L != 0 && L <= size_end - p2 && verify_hdr16(v >> 16, (uint32_t)L);
                     // record slot wc (slot kDispatchRec is a spare the emit pass never
                     // reads; a slot written as the walk stops is past its count)
-                    A.wrec[(wc < kDispatchRec ? wc : kDispatchRec) * n + k] = ((uint32_t)(p2 - cs) << 16) | (uint32_t)L;
+                    walk_record(wc, ((uint32_t)(p2 - cs) << 16) | (uint32_t)L);
                     wla = ok ? ((uint32_t)(p2 + L) | ((wc + 1u) << 18)) : wla;
                     wlb = ok ? wlb : (wlb & ~(kWalkOn << 16));
                 }
@@ -582,7 +599,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // packet, the whole datagram without the CRC field)
         auto walk_close = [&](uint32_t len) {
             if (wlb & (kWalkOwned << 16))  // (a plain datagram's record is the fix-up's: its length)
-                A.wcnt[k] = (wlb & (kWalkMerged << 16)) ? wla >> 18 : kWalkPlain;
+                walk_block((wlb & (kWalkMerged << 16)) ? wla >> 18 : kWalkPlain);
             wlb = 0u;
         };
         // after row t's boundaries: the open container's entries in row t (an
@@ -864,7 +881,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint64_t ds = segbase + (uint64_t)(int64_t)cs;
                 const int64_t size = (int64_t)(bsh + A.off[k + 1u] - ds) - 4;
                 if (!(wlb & (kWalkMerged << 16))) {
-                    A.wcnt[k] = kWalkPlain;
+                    walk_block(kWalkPlain);
                 } else {
                     int64_t pos = (int64_t)(int32_t)(wla & 0x3FFFFu) - cs;
                     uint32_t c = wla >> 18;
@@ -876,11 +893,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                         const int64_t L = (int64_t)(v & 0xFFFFu);
                         pos += 2;
                         if (L > size - pos || L == 0 || !lnl_packet_verify_hdr((uint8_t)(v >> 16), (uint64_t)L)) break;
-                        if (c < kDispatchRec) A.wrec[(size_t)c * n + k] = ((uint32_t)pos << 16) | (uint32_t)L;
+                        walk_record(c, ((uint32_t)pos << 16) | (uint32_t)L);
                         ++c;
                         pos += L;
                     }
-                    A.wcnt[k] = c;
+                    walk_block(c);
                 }
                 wlb = 0u;
             }
@@ -971,7 +988,7 @@ hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {
     const uint32_t blocks = (a.n + 255u) / 256u;
     const uint32_t prep = blocks < LNL_SPAN_PREP_BLOCKS ? blocks : LNL_SPAN_PREP_BLOCKS;
     hipLaunchKernelGGL(span_prep_kernel, dim3(prep), dim3(256), 0, stream, a);
-    if (a.wcnt)
+    if (a.wblk)
         hipLaunchKernelGGL(crc32c_span_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
     else
         hipLaunchKernelGGL(crc32c_span_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a);

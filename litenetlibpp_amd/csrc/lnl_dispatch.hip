@@ -35,6 +35,7 @@
 #include <stdint.h>
 
 #include "crc32c_kernels.h"
+#include "crc32c_span.h"
 #include "lnl_packet.h"
 
 #ifndef LNL_EXPERIMENTS
@@ -106,28 +107,42 @@ __global__ __launch_bounds__(256) void dispatch_count_kernel(DispatchArgs a) {
     a.counts[i] = c;
 }
 
-// Pass 1 of the fused path: the span kernel has walked every datagram whose
-// first byte it streamed (counts, rec); keep the counts of accepted datagrams,
-// zero the rest, and walk the few it left kWalkPending (e.g. a batch the span
-// kernel did not take).
+// Pass 1 of the fused path: the span kernel left one block per datagram
+// ([count, records 0 .. 6], written by the lane that owns the datagram; a
+// block per datagram keeps those scattered writes to one 32-byte sector).
+// Keep the counts of accepted datagrams, zero the rest, move the records to
+// the slot-major layout the emit pass reads (coalesced here), and walk again
+// what a block cannot hold (8 or more packets) or what the span kernel did not
+// see (a batch it does not take, span_runs).
 __global__ __launch_bounds__(256) void dispatch_fix_kernel(DispatchArgs a) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= a.n) return;
     const uint8_t st = a.status[i];
-    uint32_t c = a.counts[i];
-    if (st != 1u) {
-        c = 0;
-    } else if (c == kWalkPlain) {  // the datagram itself, CRC stripped
-        a.rec[i] = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
-        c = 1;
-    } else if (c == kWalkPending) {
-        const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
-        const uint32_t size = (uint32_t)(o1 - o0) - 4u;
-        uint32_t k = 0;
-        c = walk(a, o0 - a.off0, size, [&](uint32_t pos, uint32_t len) {
-            if (k < kDispatchRec) a.rec[(size_t)k * a.n + i] = (pos << 16) | len;
-            ++k;
-        });
+    uint32_t c = 0;
+    if (st == 1u) {
+        const uint64_t b = (uint64_t)(uintptr_t)a.base - a.off0;
+        const bool walked = span_runs(span_geometry(b + a.off[0], b + a.off[a.n], a.span_waves), a.span_waves);
+        const uint4* blk = reinterpret_cast<const uint4*>(a.blk + (size_t)i * kWalkBlock);
+        const uint4 b0 = walked ? blk[0] : make_uint4(kWalkBlock, 0u, 0u, 0u);
+        c = b0.x;
+        if (c == kWalkPlain) {  // the datagram itself, CRC stripped
+            a.rec[i] = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
+            c = 1;
+        } else if (c < kWalkBlock) {
+            const uint4 b1 = blk[1];
+            const uint32_t r[7] = {b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+            for (uint32_t k = 0; k < 7; ++k)
+                if (k < c) a.rec[(size_t)k * a.n + i] = r[k];
+        } else {
+            const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
+            const uint32_t size = (uint32_t)(o1 - o0) - 4u;
+            uint32_t k = 0;
+            c = walk(a, o0 - a.off0, size, [&](uint32_t pos, uint32_t len) {
+                if (k < kDispatchRec) a.rec[(size_t)k * a.n + i] = (pos << 16) | len;
+                ++k;
+            });
+        }
     }
     a.counts[i] = c;
 }
