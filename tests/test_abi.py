@@ -126,6 +126,16 @@ def test_batch_entry_points_refuse_without_gpu(pkg):
     assert list(out) == [0, 0, 0, 0]
     assert L.lnl_crc32c_batch_host_multi(ctypes.addressof(buf), ctypes.addressof(off), 4, ctypes.addressof(out),
                                          None, 0) == -22
+    # the fused filter + dispatch: n == 0 needs the device for its total only
+    # after the argument checks; a missing total is refused first
+    tot = (ctypes.c_uint32 * 1)(7)
+    st = (ctypes.c_uint8 * 4)()
+    assert L.lnl_inbound_filter_dispatch_csr_dev(ctypes.addressof(buf), ctypes.addressof(off), 4,
+                                                 ctypes.addressof(st), None, None, None, 0, None, None) == -22
+    rc = L.lnl_inbound_filter_dispatch_csr_dev(ctypes.addressof(buf), ctypes.addressof(off), 4, ctypes.addressof(st),
+                                               None, None, None, 0, ctypes.addressof(tot), None)
+    assert rc == -19, rc
+    assert list(st) == [0, 0, 0, 0] and tot[0] == 7
 
 
 def test_product_library_has_no_experiment_knobs(pkg):

@@ -651,6 +651,32 @@ def test_filter_dispatch_fused(P, n):
     assert sum(1 for (_, pos, _) in exp if pos > 0) > n // 10
 
 
+def test_filter_dispatch_fused_edges(P):
+    """Fused call at the edges: no datagrams (total 0), a small batch (the two
+    calls underneath), and a large one whose offsets start mid-buffer with the
+    buffer itself at an odd address."""
+    layer = P.Crc32cLayer()
+    rng = np.random.default_rng(5151)
+    d0 = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    st, s0, l0, p0 = P.filter_dispatch(d0, torch.zeros(1, dtype=torch.int64, device="cuda"))
+    assert st.numel() == 0 and s0.numel() == 0
+    sub = lambda m: bytes([0x00]) + rng.integers(0, 256, m - 1, dtype=np.uint8).tobytes()
+    for n, lead, shift in ((300, 0, 0), (30000, 77, 3)):
+        wires = [bytes(layer.process_outbound(_merged(rng, [sub(int(rng.integers(1, 300)))
+                                                            for _ in range(int(rng.integers(0, 7)))], "ok")))
+                 for _ in range(n)]
+        off = np.concatenate([[0], np.cumsum([len(w) for w in wires])]).astype(np.uint64) + np.uint64(lead)
+        blob = np.frombuffer(bytes(shift + lead) + b"".join(wires) + bytes(9), np.uint8)
+        d = dev(blob)[shift:]
+        o = dev(off.view(np.int64), torch.int64)
+        status, start, length, parent = P.filter_dispatch(d, o)
+        st2 = P.inbound_filter(d, o)
+        s2, l2, p2 = P.dispatch(d, o, st2)
+        assert torch.equal(status, st2)
+        assert torch.equal(start, s2) and torch.equal(length, l2) and torch.equal(parent, p2)
+        assert int((status == 1).sum()) == n
+
+
 def test_filter_dispatch_fused_shapes(P):
     """Fused path, container shapes at the walk's edges: > 8 entries (emit
     walks again), datagrams >= 64 KiB (16-bit records), many 1..3-byte
