@@ -64,11 +64,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "dispatch", "append", "filter_dispatch",
-                                           "filter_then_dispatch"], default="fixed",
+    ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "xor_csr", "dispatch", "append",
+                                           "filter_dispatch", "filter_then_dispatch"], default="fixed",
                     help="fixed: config 2 (the headline; config 4 at N = 8); csr: config 3; filter: the "
                          "batched inbound filter (CRC check + net_packet::verify) over the config-3 batch as "
-                         "wire datagrams; xor: the XOR-encryption layer in place over the config-2 batch; "
+                         "wire datagrams; xor: the XOR-encryption layer in place over the config-2 batch "
+                         "(xor_csr: over the config-3 batch); "
                          "dispatch: lnl_dispatch_csr_dev over accepted MERGED containers of 256-B "
                          "messages (the config-1 traffic shape); filter_dispatch: the same containers as wire "
                          "datagrams through lnl_inbound_filter_dispatch_csr_dev (one pass: the walk in the "
@@ -137,6 +138,8 @@ def make_workload(args, rank, world, device):
     off[1:] = torch.cumsum(lens, 0)
     total = int(off[-1].item())
     data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=device, generator=g)
+    if args.workload == "xor_csr":  # read + write every byte in place, per-datagram key phase
+        return dict(data=data, n=n, L=None, off=off, payload=total, algo=2 * total + 8 * (n + 1), xor=True)
     if args.workload == "filter":  # status byte out instead of a CRC word
         return dict(data=data, n=n, L=None, off=off, payload=total, algo=total + n + 8 * (n + 1), filter=True)
     if args.workload == "append":  # the outbound layer: payload || LE32(crc) per datagram into a wire burst
@@ -211,6 +214,8 @@ def launch(P, w, out, stream):
             w["data"].data_ptr(), w["off"].data_ptr(), w["n"], w["status"].data_ptr(),
             w["pkt_start"].data_ptr(), w["pkt_len"].data_ptr(), w["pkt_parent"].data_ptr(), w["pkts"],
             w["total"].data_ptr(), stream.cuda_stream), "lnl_dispatch_csr_dev")
+    elif w.get("xor") and w["off"] is not None:
+        P.xor_layer_csr(w["data"], w["off"], XOR_KEY, stream=stream)
     elif w.get("xor"):
         P.xor_layer_fixed(w["data"], w["L"], w["L"], w["n"], XOR_KEY, stream=stream)
     elif w.get("filter"):
@@ -494,6 +499,7 @@ def main():
             "csr": "config3: 2^20 mixed-length datagrams (64..1400 B uniform) per GPU, CSR int64 offsets",
             "filter": "config-3 batch as wire datagrams through lnl_inbound_filter_csr_dev",
             "xor": "XOR layer over the config-2 batch, in place (22-byte key)",
+            "xor_csr": "XOR layer over the config-3 batch (CSR, 64..1400 B), in place (22-byte key)",
             "dispatch": "2^20 accepted MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire), "
                         "lnl_dispatch_csr_dev",
             "filter_dispatch": "2^20 MERGED containers x 5 UNRELIABLE 256-B messages (1300 B wire) through "
@@ -507,6 +513,7 @@ def main():
                        "csr": "CRC32C GB/s (device-resident) over 1M mixed-length (64-1400B) packets; bit-exact",
                        "filter": "inbound filter GB/s (CRC check + verify, device-resident) over 1M mixed-length (64-1400B) datagrams",
                        "xor": "XOR-layer GB/s (device-resident, in place) over 1M x 1400B packets",
+                       "xor_csr": "XOR-layer GB/s (device-resident, in place) over 1M mixed-length (64-1400B) packets",
                        "dispatch": "dispatch GB/s (MERGED containers cut on device) over 1M x 1300B datagrams",
                        "filter_dispatch": "filter + dispatch GB/s (CRC check, verify, MERGED cut; device-resident) over 1M x 1300B datagrams",
                        "filter_then_dispatch": "filter + dispatch GB/s (two calls; device-resident) over 1M x 1300B datagrams",

@@ -921,6 +921,16 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
         hipError_t e = lnl::launch_xor_flat(a, f, (int)grid, flat_v, (hipStream_t)hip_stream);
         return e == hipSuccess ? 0 : hip_fail(e, "xor flat launch");
     }
+    // CSR batches: the flat CSR kernel (whole pieces per lane over the batch's
+    // byte range; the range has no gaps, so no byte outside a datagram is
+    // written except by the two edge pieces' byte stores)
+#ifndef LNL_XOR_CSR_FLAT
+#define LNL_XOR_CSR_FLAT 1
+#endif
+    if (LNL_XOR_CSR_FLAT && d_off) {
+        hipError_t e = lnl::launch_xor_csr_flat(a, S->cus * 8, (hipStream_t)hip_stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "xor csr flat launch");
+    }
     // lnl::kXorPerWg datagrams per workgroup (uncapped grid: measured faster than persistent)
     const uint32_t wgs = (n + lnl::kXorPerWg - 1u) / lnl::kXorPerWg;
 #ifndef LNL_XOR_WG_PER_CU

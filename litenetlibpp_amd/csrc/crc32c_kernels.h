@@ -269,6 +269,9 @@ struct FlatArgs {
     uint32_t sd, sr, srk;     // one grid-stride step of 16 T bytes: / S, % S, (% S) % K
 };
 hipError_t launch_xor_flat(const XorArgs& a, const FlatArgs& f, int grid, int variant, hipStream_t stream);
+// flat CSR XOR (lnl_xor.hip): consecutive lanes own whole 16-byte pieces of the
+// batch's byte range; `grid` workgroups of 256 threads, each wave a run of chunks
+hipError_t launch_xor_csr_flat(const XorArgs& a, int grid, hipStream_t stream);
 
 // Delivered packets of a filtered burst (lnl_dispatch.hip): accepted
 // datagrams, MERGED containers cut into their packets.

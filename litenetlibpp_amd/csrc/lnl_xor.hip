@@ -257,7 +257,166 @@ __global__ __launch_bounds__(kThreads) void xor_flat_kernel(XorArgs a, FlatArgs 
     }
 }
 
+// ---- flat CSR kernel -----------------------------------------------------
+// A CSR batch's bytes [off[0], off[n]) are one range with no gaps, so the flat
+// form carries over: 16-byte pieces of the range (aligned to the buffer); a
+// wave takes CHUNKS of kCsrChunkPieces consecutive pieces (lane l: pieces l,
+// l + 64, ..., coalesced dwordx4 loads and stores, nontemporal) from a contiguous
+// run of chunks, and every piece has exactly one owner -- whole-piece stores,
+// byte stores only for the batch's two edge pieces (their outside bytes are
+// not the batch's).  The key phase of a piece needs its datagram: a wave finds
+// the datagram holding its first chunk's first byte by a 64-ary search of the
+// offsets (4 rounds for 2^20 datagrams), loads the next 64 datagram starts per
+// chunk into LDS, and each lane places its piece among them by a 6-step
+// search; the next chunk's datagram follows from the count of starts.  A piece
+// with datagram starts inside it gets its key by segments (the key stream at
+// phase 0 from each start on).  A chunk holding 64 starts or more (datagrams
+// of < 32 bytes on average) reads the starts from global memory instead.
+#ifndef LNL_XOR_CSR_U
+#define LNL_XOR_CSR_U 2  // pieces per lane and chunk (2: 368 us per config-3 batch, 4: 382, 8: 444)
+#endif
+constexpr uint32_t kCsrU = LNL_XOR_CSR_U;
+constexpr uint32_t kCsrChunkPieces = 64 * kCsrU;  // 2 KiB per wave and chunk
+constexpr uint32_t kCsrChunkBytes = 16 * kCsrChunkPieces;
+
+// x % K for x < 2^32, M = ceil(2^32 / K) (64-bit: 2^32 for K = 1): the
+// quotient estimate is floor(x / K) or one more
+__device__ inline uint32_t mod_k(uint64_t x, uint32_t K, uint64_t M) {
+    const uint32_t x32 = (uint32_t)x;
+    const uint32_t q = (uint32_t)(((uint64_t)x32 * M) >> 32);
+    int64_t r = (int64_t)x32 - (int64_t)q * K;
+    if (r < 0) r += K;
+    if (r >= (int64_t)K) r -= K;
+    return (uint32_t)r;
+}
+
+// max{d <= n : pos(off[d]) <= P} by a 64-ary search over the wave (P inside
+// the batch: the result is < n); pos(x) = x - off0 + ab
+__device__ inline uint32_t wave_datagram_of(const XorArgs& a, uint64_t ab, uint64_t P) {
+    const uint32_t lane = __lane_id();
+    uint32_t lo = 0, hi = a.n;  // pos(off[lo]) <= P; answer in [lo, hi)
+    while (hi - lo > 1u) {
+        const uint32_t step = (hi - lo + 63u) >> 6;
+        const uint32_t idx = lo + lane * step;
+        const bool le = idx < hi && a.off[idx] - a.off0 + ab <= P;
+        const uint64_t m = __ballot(le);                  // lane 0 is always set
+        const uint32_t last = 63u - (uint32_t)__builtin_clzll(m);
+        lo += last * step;
+        const uint32_t nh = lo + step;
+        hi = nh < hi ? nh : hi;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void xor_csr_flat_kernel(XorArgs a, uint64_t M) {
+    __shared__ uint32_t ks[4][kKeyWords];
+    __shared__ uint32_t bnd[4][64];  // per wave: the chunk's next 64 datagram starts, chunk-relative
+    stage_key(a, ks);
+    __syncthreads();
+    const uint32_t K = a.key_len;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t ab = (uint64_t)((uintptr_t)a.base & 15u);  // buffer misalignment
+    uint8_t* const abase = a.base - ab;                       // 16-byte aligned
+    const uint64_t B0 = a.off[0] - a.off0 + ab, B1 = a.off[a.n] - a.off0 + ab;  // the batch, from abase
+    if (B1 <= B0) return;
+    const uint64_t S = B0 & ~(uint64_t)15;
+    const uint64_t chunks = (B1 - S + kCsrChunkBytes - 1u) / kCsrChunkBytes;
+    const uint64_t waves = (uint64_t)gridDim.x * 4u, gw = (uint64_t)blockIdx.x * 4u + w;
+    const uint64_t per = (chunks + waves - 1u) / waves;
+    const uint64_t c_begin = gw * per, c_end = c_begin + per < chunks ? c_begin + per : chunks;
+    if (c_begin >= c_end) return;
+    auto pos = [&](uint32_t d) -> uint64_t { return a.off[d] - a.off0 + ab; };
+    uint64_t C0 = S + c_begin * kCsrChunkBytes;
+    uint32_t d0 = wave_datagram_of(a, ab, C0 < B0 ? B0 : C0);  // holds the chunk's first batch byte
+    for (uint64_t c = c_begin; c < c_end; ++c, C0 += kCsrChunkBytes) {
+        const uint64_t Cend = C0 + kCsrChunkBytes;
+        u32x4 v[kCsrU];
+        uint64_t q[kCsrU];
+#pragma unroll
+        for (int u = 0; u < (int)kCsrU; ++u) {
+            q[u] = C0 + 16u * (lane + 64u * u);
+            if (q[u] >= B0 && q[u] + 16u <= B1)
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(abase + q[u]));
+        }
+        const uint64_t st0 = pos(d0);  // start of the datagram holding the chunk's first batch byte
+        const uint32_t dj = d0 + 1u + lane;
+        const uint64_t sj = dj <= a.n ? pos(dj) : ~0ull;
+        bnd[w][lane] = sj < Cend ? (uint32_t)(sj - C0) : kCsrChunkBytes + 1u;
+        const uint64_t in_chunk = __ballot(sj < Cend);
+        const bool many = (in_chunk >> 63) != 0ull;  // the 64th start is still inside: read starts globally
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < (int)kCsrU; ++u) {
+            const uint64_t qa = q[u];
+            if (qa >= B1 || qa + 16u <= B0) continue;  // piece outside the batch
+            const uint64_t first_byte = qa < B0 ? B0 : qa;
+            // datagram d of the piece's first batch byte, its start, and the
+            // starts after it (LDS when the chunk has < 64 of them)
+            uint32_t d;
+            if (!many) {
+                const uint32_t r = (uint32_t)(first_byte - C0);
+                uint32_t lo = 0;  // starts <= r among bnd[0..63] (sorted; beyond-chunk ones are > any r)
+#pragma unroll
+                for (uint32_t step = 32; step; step >>= 1)
+                    if (bnd[w][lo + step - 1u] <= r) lo += step;
+                d = d0 + lo;
+            } else {  // this lane's own binary search of the offsets
+                uint32_t lo = 0, hi = a.n;
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pos(mid) <= first_byte) lo = mid; else hi = mid;
+                }
+                d = lo;
+            }
+            auto start_of = [&](uint32_t dd) -> uint64_t {  // dd in (d0, d0 + 64]: LDS, else global
+                if (!many && dd > d0 && dd <= d0 + 64u) {
+                    const uint32_t rel = bnd[w][dd - d0 - 1u];
+                    return rel <= kCsrChunkBytes ? C0 + rel : (dd <= a.n ? pos(dd) : ~0ull);
+                }
+                return dd <= a.n ? pos(dd) : ~0ull;
+            };
+            const uint64_t sd = d == d0 ? st0 : start_of(d);
+            // key by segments: bytes before the next start at d's phase, then
+            // each further datagram from phase 0
+            uint32_t ph = qa >= sd ? mod_k(qa - sd, K, M) : (K - mod_k(sd - qa, K, M)) % K;
+            u32x4 key = {0u, 0u, 0u, 0u};
+            int lo_b = 0;
+            uint32_t dd = d;
+            while (true) {
+                const uint64_t nb = start_of(dd + 1u);
+                const int hi_b = nb >= qa + 16u ? 16 : (int)(nb - qa);
+                if (hi_b > lo_b) key |= key_at(ks, ph) & byte_range(lo_b, hi_b);
+                if (hi_b >= 16 || dd + 1u >= a.n) break;
+                lo_b = hi_b > lo_b ? hi_b : lo_b;
+                ph = (K - (uint32_t)lo_b % K) % K;  // byte lo_b gets key[0]
+                ++dd;
+            }
+            if (qa >= B0 && qa + 16u <= B1) {
+                __builtin_nontemporal_store(v[u] ^ key, reinterpret_cast<u32x4*>(abase + qa));
+            } else {  // the batch's edge piece: its own bytes only
+                uint8_t* bp = abase + qa;
+                for (uint32_t j = 0; j < 16u; ++j) {
+                    const uint64_t at = qa + j;
+                    if (at >= B0 && at < B1) bp[j] ^= (uint8_t)(key[j >> 2] >> (8 * (j & 3)));
+                }
+            }
+        }
+        // the next chunk's first datagram: the last start <= Cend
+        if (!many)
+            d0 += (uint32_t)__popcll(__ballot(sj <= Cend));
+        else if (c + 1u < c_end)
+            d0 = wave_datagram_of(a, ab, Cend);
+        __builtin_amdgcn_wave_barrier();  // bnd[w] is rewritten by the next chunk
+    }
+}
+
 }  // namespace
+
+hipError_t launch_xor_csr_flat(const XorArgs& a, int grid, hipStream_t stream) {
+    const uint64_t M = ((1ull << 32) + a.key_len - 1u) / a.key_len;
+    hipLaunchKernelGGL(xor_csr_flat_kernel, dim3(grid), dim3(kThreads), 0, stream, a, M);
+    return hipGetLastError();
+}
 
 hipError_t launch_xor_flat(const XorArgs& a, const FlatArgs& f, int grid, int variant, hipStream_t stream) {
 #if !LNL_EXPERIMENTS

@@ -723,6 +723,34 @@ def test_xor_layer_csr(P, klen):
     assert np.array_equal(d.cpu().numpy(), data)
 
 
+@pytest.mark.parametrize("shift", [0, 5])
+def test_xor_layer_csr_dense_and_misaligned(P, shift):
+    """The flat CSR kernel's other cases: runs of tiny and empty datagrams
+    (chunks holding 64 or more datagram starts: the global-memory path), a
+    buffer at an odd address, a batch ending mid-piece, and a batch whose
+    first chunk starts before its first byte."""
+    rng = np.random.default_rng(77 + shift)
+    key = rng.integers(0, 256, 23, dtype=np.uint8).tobytes()
+    n = 30000
+    lens = rng.integers(0, 1433, n)
+    lens[5000:6000] = rng.integers(0, 12, 1000)    # ~6 KB of starts every few bytes
+    lens[20000:20300] = 0                          # a run of empty datagrams
+    lead = 9
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(lead)
+    data = rng.integers(0, 256, shift + int(off[-1]) + 7, dtype=np.uint8)
+    d = dev(data)[shift:]
+    o = dev(off.view(np.int64), torch.int64)
+    P.xor_layer_csr(d, o, key)
+    got = d.cpu().numpy()
+    src = data[shift:]
+    exp = src.copy()
+    for i in range(n):
+        a, b = int(off[i]), int(off[i + 1])
+        exp[a:b] = oracle.xor_layer(src[a:b], key)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"
+
+
 @pytest.mark.parametrize("stride,length,klen,shift", [
     (1400, 1400, 10, 0), (1408, 1400, 10, 0), (64, 17, 10, 0), (1432, 1, 10, 0),
     (16, 16, 3, 0), (17, 17, 256, 0), (17, 5, 1, 0), (33, 32, 37, 0), (1400, 1400, 22, 0),

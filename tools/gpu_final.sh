@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -1 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && tail -1 gpurun_out/smoke.log || exit 1
 timeout -k 10 300 python -u bench.py > gpurun_out/final_fixed.json 2> gpurun_out/final_fixed.err || exit 1
-for w in csr filter xor dispatch append filter_dispatch filter_then_dispatch; do
+for w in csr filter xor xor_csr dispatch append filter_dispatch filter_then_dispatch; do
   timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline --no-host-path > gpurun_out/final_$w.json 2> gpurun_out/final_$w.err || exit 1
 done
 timeout -k 10 300 python -u bench.py --workload csr > gpurun_out/final_csr_host.json 2> gpurun_out/final_csr_host.err || exit 1

@@ -35,6 +35,9 @@ VARIANTS = {
     "prep8k": "-DLNL_SPAN_PREP_BLOCKS=8192u",       # span pre-pass: 8192 workgroups (before: 1 % slower than 1024)
     "prep256": "-DLNL_SPAN_PREP_BLOCKS=256u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
+    "xcsr_u4": "-DLNL_XOR_CSR_U=4",                 # flat CSR XOR: 4 pieces per lane and chunk (4 KiB)
+    "xcsr_u8": "-DLNL_XOR_CSR_U=8",                 # ... 8 (8 KiB)
+    "xcsr_old": "-DLNL_XOR_CSR_FLAT=0",             # CSR XOR: the per-datagram kernel (before)
     "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)
     "walk_noend": "-DLNL_WALK_DIAG=2",              # ... no walk at datagram ends (wrong packets)
     "walk_notail": "-DLNL_WALK_DIAG=4",             # ... no global-memory finish (wrong packets)
@@ -180,6 +183,22 @@ def run(names, rounds, workloads):
             def call(L):
                 L.lnl_crc32c_append_csr_dev(data.data_ptr(), off.data_ptr(), n_pk, wire.data_ptr(), out.data_ptr(),
                                             s.cuda_stream)
+        elif wl[0] == "xorcsr":  # ("xorcsr", n): XOR layer in place over a config-3-shaped CSR batch
+            n_pk = wl[1]
+            lens = torch.randint(64, 1401, (n_pk,), device=dev, generator=g, dtype=torch.int64)
+            off = torch.zeros(n_pk + 1, dtype=torch.int64, device=dev)
+            off[1:] = torch.cumsum(lens, 0)
+            total = int(off[-1])
+            data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+            algo = 2 * total + 8 * (n_pk + 1)
+            wkey = f"xorcsr{n_pk}"
+            key = b"LiteNetLibPP-bench-key"
+            for L in libs.values():
+                L.lnl_xor_layer_csr_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                    ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
+
+            def call(L):
+                L.lnl_xor_layer_csr_dev(data.data_ptr(), off.data_ptr(), n_pk, key, len(key), s.cuda_stream)
         elif wl[0] == "fd":  # ("fd", n): filter + dispatch over n MERGED containers of 5 x 256-B packets
             n_pk = wl[1]
             S = 1 + 5 * 259 + 4
@@ -250,7 +269,7 @@ def main():
     if a.cmd == "build":
         build(names)
     else:
-        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.split(":")[0] in ("csr", "xor", "append", "filter", "fd")
+        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.split(":")[0] in ("csr", "xor", "append", "filter", "fd", "xorcsr")
               else tuple(int(v) for v in w.split(":")) for w in a.workloads.split(",")]
         res = run(names, a.rounds, wl)
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
