@@ -37,7 +37,8 @@ VARIANTS = {
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
     "xcsr_u4": "-DLNL_XOR_CSR_U=4",                 # flat CSR XOR: 4 pieces per lane and chunk (4 KiB)
     "xcsr_u8": "-DLNL_XOR_CSR_U=8",                 # ... 8 (8 KiB)
-    "xcsr_old": "-DLNL_XOR_CSR_FLAT=0",             # CSR XOR: the per-datagram kernel (before)
+    "xcsr_old": "-DLNL_XOR_CSR_FLAT=0",
+    "xcsr_prev": "",                                # A/B slot: built from another lnl_xor.hip copied in by hand             # CSR XOR: the per-datagram kernel (before)
     "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)
     "walk_noend": "-DLNL_WALK_DIAG=2",              # ... no walk at datagram ends (wrong packets)
     "walk_notail": "-DLNL_WALK_DIAG=4",             # ... no global-memory finish (wrong packets)
