@@ -13,7 +13,7 @@ done
 timeout -k 10 300 python -u bench.py --workload csr > gpurun_out/final_csr_host.json 2> gpurun_out/final_csr_host.err || exit 1
 timeout -k 10 300 env LNL_BENCH_BACKEND=gloo LNL_BENCH_ONE_GPU=1 python -u bench.py --gpus 2 --no-cpu-baseline > gpurun_out/final_fixed_2ranks.json 2> gpurun_out/final_fixed_2ranks.err || exit 1
 # summaries on the box (the rocprof databases are too big to copy back)
-for w in fixed csr filter dispatch xor append filter_dispatch; do
+for w in fixed csr filter dispatch xor xor_csr append filter_dispatch; do
   timeout -k 10 900 bash tools/profile_round.sh $TAG $w || exit 1
   PROFILES_DIR=gpurun_out/profiles_$TAG python3 tools/write_profiles.py $TAG $w > /dev/null || exit 1
   rm -rf gpurun_out/prof_${TAG}_$w
