@@ -23,7 +23,7 @@ from prof_summary import from_db, short  # noqa: E402
 # kernels of liblnl_crc32c.so (rocprofv3 names contain these)
 PRODUCT_KERNELS = ("crc32c_", "bucket_count", "bucket_scatter", "bucket_hist", "bucket_scan", "bucket_place",
                    "pair_count", "pair_scatter", "seg_prep", "seg_fixup", "verify_from_wire", "csr_plan",
-                   "dispatch_", "xor_layer", "xor_flat", "span_prep", "append_kernel")
+                   "dispatch_", "xor_layer", "xor_flat", "xor_csr_flat", "span_prep", "append_kernel")
 
 
 def main():
