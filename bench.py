@@ -329,7 +329,10 @@ def cpu_baseline(w, host):
     if quota:
         cores = min(cores, quota)
     res, ref = {}, None
-    for th in (1, cores):
+    nproc = os.cpu_count() or cores
+    # 1 core, the job's share, and -- for the record -- one thread per CPU the
+    # machine reports (beyond the share they only time-slice)
+    for th in sorted({1, cores, nproc}):
         times = []
         t_end = time.perf_counter() + 2.0
         while True:
@@ -584,6 +587,8 @@ def main():
                 "sample": f"the whole batch ({w['n']} datagrams, {w['payload'] / 1e9:.3f} GB, copied to host "
                           f"memory untimed); oracle SSE4.2 crc32 loop, OpenMP, median of repeats over ~2 s",
                 "single_core_value": round(res[1], 3),
+                "all_cpus_value": round(res.get(os.cpu_count() or cores, res[cores]), 3),
+                "all_cpus_threads": os.cpu_count(),
                 "nproc": os.cpu_count(),
                 "affinity_cpus": len(os.sched_getaffinity(0)),
                 "cgroup_cpu_quota": quota,
