@@ -823,7 +823,7 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     if (cap && (!d_pkt_start || !d_pkt_len || !d_pkt_parent)) return fail(-EINVAL, "NULL output");
     DeviceState* S;
     if (int rc = current_device(&S)) return rc;
-    // (records are indexed slot * n + i in 32 bits)
+    // (the span kernel indexes walk blocks as 8 k in 32 bits)
     if (n < LNL_BUCKET_MIN_N || n > (1u << 28) || csr_path() != kPathBucketed) {
         if (int rc = lnl_inbound_filter_csr_dev(d_base, d_off, n, d_status, hip_stream)) return rc;
         return lnl_dispatch_csr_dev(d_base, d_off, n, d_status, d_pkt_start, d_pkt_len, d_pkt_parent, cap, d_total,

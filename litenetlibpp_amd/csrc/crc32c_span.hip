@@ -299,7 +299,7 @@ struct Transpose<8> {
     __device__ static LNL_INLINE void write(uint32_t, uint32_t, const u32x4*) {}
 };
 
-// one byte of a 4-byte-aligned pair of dwords: bytes q[0..2] (global memory;
+// bytes q[0..2] (LE) from the aligned pair of dwords holding them (global memory;
 // see lnl_dispatch.hip load3 for why both dwords are inside the batch)
 __device__ LNL_INLINE uint32_t global_load3(uint64_t q) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(q & ~(uint64_t)3);
