@@ -319,6 +319,9 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 }
 #endif  // LNL_EXPERIMENTS
 
+#ifndef LNL_SPAN_ROUNDS
+#define LNL_SPAN_ROUNDS 1u  // wave-batches per resident wave the segment length is chosen for (experiments)
+#endif
 #ifndef LNL_SPAN_FIX_WGS
 #define LNL_SPAN_FIX_WGS 0xFFFFFFFFu  // cap on the batch kernel's grid after the span kernel (experiments)
 #endif
@@ -338,7 +341,7 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
     g.off = a.off;
     g.off0 = a.off0;
     g.n = a.n;
-    g.waves = (uint32_t)S.cus * (uint32_t)(lnl::kSpanThreads / 64);
+    g.waves = (uint32_t)S.cus * (uint32_t)(lnl::kSpanThreads / 64) * LNL_SPAN_ROUNDS;
     g.out = a.out;
     g.tab = S.span_tab;
     void* scratch = nullptr;

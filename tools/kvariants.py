@@ -39,6 +39,7 @@ VARIANTS = {
     "xcsr_u8": "-DLNL_XOR_CSR_U=8",                 # ... 8 (8 KiB)
     "xcsr_old": "-DLNL_XOR_CSR_FLAT=0",
     "xcsr_prev": "",                                # A/B slot: built from another lnl_xor.hip copied in by hand             # CSR XOR: the per-datagram kernel (before)
+    "span_r2": "-DLNL_SPAN_ROUNDS=2u",              # CSR span: segments for two wave-batches per wave (static)
     "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)
     "walk_noend": "-DLNL_WALK_DIAG=2",              # ... no walk at datagram ends (wrong packets)
     "walk_notail": "-DLNL_WALK_DIAG=4",             # ... no global-memory finish (wrong packets)
