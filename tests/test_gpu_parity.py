@@ -751,6 +751,34 @@ def test_xor_layer_csr_dense_and_misaligned(P, shift):
     assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"
 
 
+def test_xor_layer_csr_runs_of_chunks(P):
+    """A batch of ~220 MB: every wave of the flat CSR kernel takes a run of
+    chunks (the next chunk's datagram carried from the count of starts, or
+    searched again after a dense chunk), checked byte for byte against the
+    restatement, vectorised."""
+    rng = np.random.default_rng(4321)
+    key = rng.integers(0, 256, 22, dtype=np.uint8)
+    n = 300000
+    lens = rng.integers(64, 1401, n)
+    for s0 in (1000, 150000, 297000):               # dense stretches inside the runs
+        lens[s0:s0 + 2000] = rng.integers(0, 24, 2000)
+    lead = 3
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) + lead
+    total = int(off[-1]) + 5
+    g = torch.Generator(device="cuda")
+    g.manual_seed(17)
+    d = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=g)
+    src = d.cpu().numpy()
+    o = dev(off.view(np.int64), torch.int64)
+    P.xor_layer_csr(d, o, key.tobytes())
+    got = d.cpu().numpy()
+    phase = np.arange(int(off[-1]) - lead, dtype=np.int64) - np.repeat(off[:-1] - lead, lens)
+    exp = src.copy()
+    exp[lead:int(off[-1])] ^= key[phase % key.size]
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"
+
+
 @pytest.mark.parametrize("stride,length,klen,shift", [
     (1400, 1400, 10, 0), (1408, 1400, 10, 0), (64, 17, 10, 0), (1432, 1, 10, 0),
     (16, 16, 3, 0), (17, 17, 256, 0), (17, 5, 1, 0), (33, 32, 37, 0), (1400, 1400, 22, 0),
