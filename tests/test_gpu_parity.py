@@ -677,6 +677,38 @@ def test_filter_dispatch_fused_edges(P):
         assert int((status == 1).sum()) == n
 
 
+def test_filter_dispatch_fused_several_batches_per_wave(P):
+    """Fused call over ~2.3 GB of 1300-byte containers (five 256-byte packets
+    each, some plain datagrams, some corrupted): waves take several
+    wave-batches; statuses and packets equal the two calls'."""
+    n = 1_750_000
+    S = 1 + 5 * 259 + 4
+    g = torch.Generator(device="cuda")
+    g.manual_seed(2024)
+    data = torch.randint(0, 256, (n * S,), dtype=torch.uint8, device="cuda", generator=g)
+    d2 = data.view(n, S)
+    plain = torch.rand(n, device="cuda", generator=g) < 0.1
+    d2[:, 0] = torch.where(plain, torch.tensor(0x01, dtype=torch.uint8, device="cuda"),
+                           torch.tensor(0x0C, dtype=torch.uint8, device="cuda"))
+    for j in range(5):
+        b = 1 + 259 * j
+        d2[:, b] = 1
+        d2[:, b + 1] = 1
+        d2[:, b + 2] = 0
+    crc = P.batch_fixed(data, S, S - 4, n)
+    d2[:, S - 4:] = crc.view(torch.uint8).view(n, 4)
+    bad_rows = torch.nonzero(torch.rand(n, device="cuda", generator=g) < 0.02).flatten()
+    d2[bad_rows, 7] ^= 0x10
+    off = torch.arange(0, (n + 1) * S, S, dtype=torch.int64, device="cuda")
+    status, start, length, parent = P.filter_dispatch(data, off)
+    st2 = P.inbound_filter(data, off)
+    s2, l2, p2 = P.dispatch(data, off, st2)
+    assert torch.equal(status, st2)
+    assert int((status == 1).sum()) == n - bad_rows.numel()
+    assert torch.equal(parent, p2) and torch.equal(start, s2) and torch.equal(length, l2)
+    del data, d2
+
+
 def test_filter_dispatch_fused_shapes(P):
     """Fused path, container shapes at the walk's edges: > 8 entries (emit
     walks again), datagrams >= 64 KiB (16-bit records), many 1..3-byte
