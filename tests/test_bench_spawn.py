@@ -48,3 +48,17 @@ def test_world_size_mismatch_is_refused():
     r = _run(["--gpus", "2", "--steps", "1"], extra_env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE" in r.stderr
+
+
+def test_every_workload_names_its_metric():
+    """Each --workload prints one line with its own metric and workload name
+    (dry run: the plumbing, no kernel)."""
+    seen = set()
+    for wl in ("fixed", "csr", "filter", "xor", "xor_csr", "dispatch", "append", "filter_dispatch",
+               "filter_then_dispatch"):
+        r = _run(["--workload", wl, "--steps", "1", "--warmup", "0", "--packets", "64"])
+        assert r.returncode == 0, (wl, r.stderr)
+        line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        assert line["n_gpus"] == 1 and line["unit"] == "GB/s" and line["higher_is_better"]
+        seen.add((line["metric"], line["config"]["workload"]))
+    assert len(seen) == 9
