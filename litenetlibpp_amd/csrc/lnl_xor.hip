@@ -273,7 +273,7 @@ __global__ __launch_bounds__(kThreads) void xor_flat_kernel(XorArgs a, FlatArgs 
 // phase 0 from each start on).  A chunk holding 64 starts or more (datagrams
 // of < 32 bytes on average) reads the starts from global memory instead.
 #ifndef LNL_XOR_CSR_U
-#define LNL_XOR_CSR_U 2  // pieces per lane and chunk (2: 368 us per config-3 batch, 4: 382, 8: 444)
+#define LNL_XOR_CSR_U 2  // pieces per lane and chunk (1: 445 us per config-3 batch, 2: 368, 4: 382, 8: 444)
 #endif
 constexpr uint32_t kCsrU = LNL_XOR_CSR_U;
 constexpr uint32_t kCsrChunkPieces = 64 * kCsrU;  // 2 KiB per wave and chunk
