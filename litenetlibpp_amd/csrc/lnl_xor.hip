@@ -308,6 +308,24 @@ __device__ inline uint32_t wave_datagram_of(const XorArgs& a, uint64_t ab, uint6
     return lo;
 }
 
+#ifndef LNL_XOR_CSR_NT
+#define LNL_XOR_CSR_NT 1  // nontemporal whole-piece loads and stores (experiments: 0 = default policy)
+#endif
+__device__ inline u32x4 csr_load(const u32x4* p) {
+#if LNL_XOR_CSR_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ inline void csr_store(u32x4 v, u32x4* p) {
+#if LNL_XOR_CSR_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 __global__ __launch_bounds__(256) void xor_csr_flat_kernel(XorArgs a, uint64_t M) {
     __shared__ uint32_t ks[4][kKeyWords];
     __shared__ uint32_t bnd[4][64];  // per wave: the chunk's next 64 datagram starts, chunk-relative
@@ -336,7 +354,7 @@ __global__ __launch_bounds__(256) void xor_csr_flat_kernel(XorArgs a, uint64_t M
         for (int u = 0; u < (int)kCsrU; ++u) {
             q[u] = C0 + 16u * (lane + 64u * u);
             if (q[u] >= B0 && q[u] + 16u <= B1)
-                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(abase + q[u]));
+                v[u] = csr_load(reinterpret_cast<const u32x4*>(abase + q[u]));
         }
         const uint64_t st0 = pos(d0);  // start of the datagram holding the chunk's first batch byte
         const uint32_t dj = d0 + 1u + lane;
@@ -392,7 +410,7 @@ __global__ __launch_bounds__(256) void xor_csr_flat_kernel(XorArgs a, uint64_t M
                 ++dd;
             }
             if (qa >= B0 && qa + 16u <= B1) {
-                __builtin_nontemporal_store(v[u] ^ key, reinterpret_cast<u32x4*>(abase + qa));
+                csr_store(v[u] ^ key, reinterpret_cast<u32x4*>(abase + qa));
             } else {  // the batch's edge piece: its own bytes only
                 uint8_t* bp = abase + qa;
                 for (uint32_t j = 0; j < 16u; ++j) {
