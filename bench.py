@@ -38,6 +38,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import datetime
 import json
 import os
 import socket
@@ -91,18 +92,38 @@ def _free_port() -> int:
 
 def spawn_ranks(n: int) -> int:
     """One child process per GPU, started before this process makes any GPU
-    call (children are fresh interpreters, never an exec of this one)."""
+    call (children are fresh interpreters, never an exec of this one).  Every
+    child is polled: the first one to exit non-zero ends the run -- its
+    siblings (which would otherwise wait in rendezvous or a barrier forever)
+    are terminated, then killed -- and its status is returned."""
     port = _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    for p in procs:
-        c = p.wait()
-        rc = rc or c
-    return rc
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0:
+                for q in live:
+                    q.terminate()
+                t_end = time.time() + 10.0
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.1, t_end - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with status {c}; "
+                                 f"stopped the other {len(live)} rank(s)\n")
+                return c
+        time.sleep(0.05)
+    return 0
 
 
 # ------------------------------------------------------------------ workloads
@@ -255,8 +276,11 @@ def hbm_probe_peak(data, device):
         nbytes = data.numel() // 8192 * 8192 if form < 2 else seg_round * waves.get(form, 8) // 8
         if nbytes > data.numel() or nbytes == 0:
             continue
+        rc = 0
         for _ in range(3):
-            L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream, form)
+            rc = rc or L.lnl_probe_stream_read(data.data_ptr(), nbytes, sink.data_ptr(), s.cuda_stream, form)
+        if rc != 0:  # a form the probe rejects: no figure rather than an empty event pair's
+            continue
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 10
         e0.record()
@@ -402,6 +426,8 @@ def main():
                  f"(torchrun --nproc-per-node {args.gpus}) or drop the launcher and let --gpus spawn them")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if DRY and os.environ.get("LNL_BENCH_DRYRUN_FAIL_RANK") == str(rank):
+        sys.exit(3)  # dry-run test knob: a rank that dies before rendezvous (spawn_ranks must not hang)
     # Rehearsal knobs (the driver never sets them): LNL_BENCH_BACKEND=gloo and
     # LNL_BENCH_ONE_GPU=1 run N ranks on one GPU to exercise the N > 1 path.
     backend = "gloo" if DRY else os.environ.get("LNL_BENCH_BACKEND", "nccl")
@@ -414,10 +440,12 @@ def main():
     red_dev = device if backend == "nccl" else None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # bounded rendezvous: a rank that never arrives ends the run, not hangs it
+        tmo = datetime.timedelta(seconds=300)
         if backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device, timeout=tmo)
         else:
-            dist.init_process_group(backend, rank=rank, world_size=world)
+            dist.init_process_group(backend, rank=rank, world_size=world, timeout=tmo)
     import litenetlibpp_amd as P
     if not DRY:
         P.lib()

@@ -18,6 +18,13 @@
 //         -Wl,-rpath,$PWD/litenetlibpp_amd -o socket_path
 //   ./socket_path [--count N] [--burst B] [--corrupt K] [--device D] [--receivers R]
 //
+// --egress 1 (the send half): the senders hold PAYLOAD
+// bursts (no CRC) and run the product's send side per burst --
+// lnl_crc32c_append_host (pinned payloads -> H2D -> CRC + append on the GPU ->
+// D2H wire burst) then one lnl_egress_send_batch (sendmmsg) -- so every byte
+// goes host -> GPU -> socket -> host -> GPU.  The line then also carries the
+// send side's times and its PCIe-inclusive append rate.
+//
 // --receivers R: R receive sockets bound to
 // one port with SO_REUSEPORT, one receiver thread each with its own pinned
 // burst buffer, fed by R sender sockets (the kernel spreads flows over the
@@ -35,6 +42,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <random>
 #include <string>
 #include <thread>
@@ -52,6 +60,7 @@ struct Opts {
     uint32_t corrupt = 50;
     int device = 0;
     uint32_t receivers = 1;
+    uint32_t egress = 0;
 };
 
 Opts parse(int argc, char** argv) {
@@ -64,6 +73,7 @@ Opts parse(int argc, char** argv) {
         else if (k == "--corrupt") o.corrupt = (uint32_t)v;
         else if (k == "--device") o.device = (int)v;
         else if (k == "--receivers") o.receivers = (uint32_t)std::max(1L, std::min(v, 64L));
+        else if (k == "--egress") o.egress = (uint32_t)v;
     }
     return o;
 }
@@ -87,11 +97,25 @@ std::vector<std::vector<uint8_t>> make_wire(uint32_t n, uint32_t corrupt) {
     return w;
 }
 
+// payloads only (header byte + body, no CRC field): the egress mode's input
+std::vector<std::vector<uint8_t>> make_payloads(uint32_t n) {
+    std::mt19937_64 rng(11);
+    std::vector<std::vector<uint8_t>> p(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        p[i].resize(1 + rng() % (LNL_INGRESS_SLOT - LNL_CRC32C_LAYER_EXTRA));
+        for (auto& b : p[i]) b = (uint8_t)rng();
+        const uint32_t r = (uint32_t)(rng() % 100);
+        p[i][0] = r < 60 ? 0x00 : r < 95 ? 0x01 : (uint8_t)(0x12 + r % 14);
+    }
+    return p;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     const Opts o = parse(argc, argv);
-    const auto wire = make_wire(o.count, o.corrupt);
+    const auto wire = o.egress ? std::vector<std::vector<uint8_t>>() : make_wire(o.count, o.corrupt);
+    const auto payloads = o.egress ? make_payloads(o.count) : std::vector<std::vector<uint8_t>>();
 
     const uint32_t R = o.receivers;
     std::vector<int> rx(R), tx(R);
@@ -119,9 +143,68 @@ int main(int argc, char** argv) {
     }
 
     std::atomic<uint32_t> senders_left{R};
+    std::atomic<int> tx_fail{0};
+    std::vector<double> t_append(R, 0.0), t_egress(R, 0.0);
+    std::vector<uint64_t> tx_payload(R, 0);
     std::vector<std::thread> senders;
     for (uint32_t r = 0; r < R; ++r)
-        senders.emplace_back([&, r] {  // sendmmsg bursts of 64 (datagrams r, r + R, ...), paced by the socket buffer
+        senders.emplace_back(o.egress ? std::function<void()>([&, r] {
+            // the product's send side per burst of 64: payloads -> pinned burst
+            // -> lnl_crc32c_append_host -> lnl_egress_send_batch
+            constexpr uint32_t kB = 64;
+            const size_t pcap = (size_t)kB * LNL_INGRESS_SLOT;
+            uint8_t *pay = nullptr, *wb = nullptr;
+            if (hipSetDevice(o.device) != hipSuccess || hipHostMalloc((void**)&pay, pcap) != hipSuccess ||
+                hipHostMalloc((void**)&wb, pcap + kB * LNL_CRC32C_LAYER_EXTRA) != hipSuccess) {
+                tx_fail = 2;
+                --senders_left;
+                return;
+            }
+            std::vector<uint64_t> poff(kB + 1), woff(kB + 1), rel(kB + 1);
+            std::vector<int64_t> st(kB);
+            std::vector<uint32_t> mine;
+            for (uint32_t i = r; i < o.count; i += R) mine.push_back(i);
+            std::mt19937 flip(r + 1);
+            for (size_t i = 0; i < mine.size() && !tx_fail;) {
+                const uint32_t k = (uint32_t)std::min<size_t>(kB, mine.size() - i);
+                poff[0] = woff[0] = 0;
+                for (uint32_t j = 0; j < k; ++j) {
+                    const auto& p = payloads[mine[i + j]];
+                    memcpy(pay + poff[j], p.data(), p.size());
+                    poff[j + 1] = poff[j] + p.size();
+                    woff[j + 1] = poff[j + 1] + (uint64_t)(j + 1) * LNL_CRC32C_LAYER_EXTRA;
+                }
+                const auto a0 = clk::now();
+                if (lnl_crc32c_append_host(pay, poff.data(), k, wb, nullptr, o.device) != 0) {
+                    fprintf(stderr, "append_host: %s\n", lnl_crc32c_last_error());
+                    tx_fail = 1;
+                    break;
+                }
+                const auto a1 = clk::now();
+                if (o.corrupt)  // a flipped bit on the wire now and then: the receiver's filter drops it
+                    for (uint32_t j = 0; j < k; ++j)
+                        if (mine[i + j] % o.corrupt == o.corrupt - 1) wb[woff[j] + flip() % (woff[j + 1] - woff[j])] ^= 0x08;
+                uint32_t done = 0;
+                while (done < k) {  // paced by the socket buffer
+                    for (uint32_t j = done; j <= k; ++j) rel[j - done] = woff[j] - woff[done];
+                    const int64_t m = lnl_egress_send_batch(tx[r], wb + woff[done], rel.data(), k - done, nullptr, 0,
+                                                            st.data(), 200);
+                    if (m < 0) {
+                        fprintf(stderr, "egress: %lld\n", (long long)m);
+                        tx_fail = 1;
+                        break;
+                    }
+                    done += (uint32_t)m;
+                }
+                t_append[r] += std::chrono::duration<double>(a1 - a0).count();
+                t_egress[r] += std::chrono::duration<double>(clk::now() - a1).count();
+                tx_payload[r] += poff[k];
+                i += k;
+            }
+            (void)hipHostFree(pay);
+            (void)hipHostFree(wb);
+            --senders_left;
+        }) : std::function<void()>([&, r] {  // sendmmsg bursts of 64 (datagrams r, r + R, ...), paced by the socket buffer
             std::vector<mmsghdr> m(64);
             std::vector<iovec> iov(64);
             std::vector<uint32_t> mine;
@@ -140,7 +223,7 @@ int main(int argc, char** argv) {
                 else std::this_thread::yield();
             }
             --senders_left;
-        });
+        }));
 
     std::atomic<uint64_t> got{0}, bytes{0}, c0{0}, c1{0}, c2{0}, mismatch{0};
     std::atomic<int> fail{0};
@@ -198,6 +281,7 @@ int main(int argc, char** argv) {
     const double wall = std::chrono::duration<double>(clk::now() - t0).count();
     for (auto& t : senders) t.join();
     if (fail) return fail.load();
+    if (tx_fail) return 10 + tx_fail.load();
     double ti = 0, tf = 0, tboth = 0;  // slowest receiver
     for (uint32_t r = 0; r < R; ++r)
         ti = std::max(ti, t_ingress[r]), tf = std::max(tf, t_filter[r]), tboth = std::max(tboth, t_ingress[r] + t_filter[r]);
@@ -206,11 +290,20 @@ int main(int argc, char** argv) {
     printf("{\"sent\": %u, \"received\": %llu, \"bytes\": %llu, \"burst\": %u, \"receivers\": %u, "
            "\"ingress_s\": %.4f, \"filter_s\": %.4f, \"wall_s\": %.4f, "
            "\"ingress_gbps\": %.3f, \"ingress_plus_gpu_filter_gbps\": %.3f, \"aggregate_wall_gbps\": %.3f, "
-           "\"accept\": %llu, \"drop_crc\": %llu, \"malformed\": %llu, \"gpu_cpu_mismatch\": %llu}\n",
+           "\"accept\": %llu, \"drop_crc\": %llu, \"malformed\": %llu, \"gpu_cpu_mismatch\": %llu",
            o.count, (unsigned long long)got.load(), (unsigned long long)bytes.load(), o.burst, R, ti, tf, wall,
            bytes.load() / ti / 1e9, bytes.load() / tboth / 1e9, bytes.load() / wall / 1e9,
            (unsigned long long)c1.load(), (unsigned long long)c0.load(), (unsigned long long)c2.load(),
            (unsigned long long)mismatch.load());
+    if (o.egress) {
+        double ta = 0, te = 0;
+        uint64_t pb = 0;
+        for (uint32_t r = 0; r < R; ++r) ta = std::max(ta, t_append[r]), te = std::max(te, t_egress[r]), pb += tx_payload[r];
+        printf(", \"egress\": true, \"tx_payload_bytes\": %llu, \"append_host_s\": %.4f, \"egress_send_s\": %.4f, "
+               "\"append_host_gbps\": %.3f, \"egress_send_gbps\": %.3f",
+               (unsigned long long)pb, ta, te, pb / (double)R / ta / 1e9, pb / (double)R / te / 1e9);
+    }
+    printf("}\n");
     for (uint32_t r = 0; r < R; ++r) close(rx[r]), close(tx[r]);
     return mismatch.load() ? 3 : 0;
 }

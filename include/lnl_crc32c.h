@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 7
+#define LNL_CRC32C_ABI_VERSION 8
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -192,6 +192,38 @@ int lnl_inbound_filter_host(const uint8_t* h_base, const uint64_t* h_off, uint32
 #define LNL_INGRESS_SLOT 1432
 int lnl_ingress_recv_batch(int fd, uint8_t* buf, size_t cap, uint64_t* off, uint32_t max_n, void* addrs,
                            int wait_ms);
+
+/* Host-resident outbound layer (the send side of the socket path; SURVEY.md
+ * 8(f) item 2): the payload burst, datagram i = h_payload[h_off[i] ..
+ * h_off[i+1]) as in lnl_crc32c_batch_host (pinned
+ * memory gives the full PCIe rate) goes H2D in chunks over two HIP streams,
+ * through lnl_crc32c_append_csr_dev on `device`, and back D2H as the wire
+ * burst: datagram i at h_wire + (h_off[i] - h_off[0]) + 4 i as
+ * payload || LE32(CRC32C(payload)) -- the bytes lnl_crc32c_layer_outbound
+ * gives for it, back to back (h_off[n] - h_off[0] + 4 n bytes; its offsets are
+ * h_off[i] - h_off[0] + 4 i).  h_crc (optional, may be NULL) receives the
+ * CRCs.  h_wire must not overlap h_payload.  Blocks until done.  This is
+ * net_manager::send_raw's layer step for a whole burst
+ * (/root/reference/src/lnl/net_manager.cpp:515-521). */
+int lnl_crc32c_append_host(const uint8_t* h_payload, const uint64_t* h_off, uint32_t n, uint8_t* h_wire,
+                           uint32_t* h_crc, int device);
+
+/* Batched socket egress (CPU): sendmmsg of the wire
+ * burst's datagrams -- datagram i = wire[off[i] .. off[i+1]), the CSR layout
+ * lnl_ingress_recv_batch produces (for lnl_crc32c_append_host's wire burst,
+ * off[i] = h_off[i] - h_off[0] + 4 i) -- in calls of up to 1024, replacing
+ * one sendto per datagram
+ * (/root/reference/src/lnl/net_manager.cpp:515-523).  addrs: NULL for a
+ * connected socket, else naddrs (1: one endpoint for all, or n: one per
+ * datagram) struct sockaddr_in.  status (optional, n entries) receives, for
+ * every datagram attempted, the bytes sent or a negative errno for a datagram
+ * the kernel refused (send_raw's error case, :525-567; the burst goes on).
+ * When the socket buffer is full, wait_ms != 0 polls for room (-1: forever)
+ * and 0 returns at once.  Returns the number of datagrams attempted, from the
+ * front (the rest were not: buffer full and the wait expired), or a negative
+ * errno when the call itself is invalid (bad fd, arguments). */
+int64_t lnl_egress_send_batch(int fd, const uint8_t* wire, const uint64_t* off, uint32_t n, const void* addrs,
+                              uint32_t naddrs, int64_t* status, int wait_ms);
 
 /* Multi-device form of lnl_crc32c_batch_host: the batch
  * is split into ndev contiguous datagram ranges of ceil(n / ndev) (the last

@@ -9,11 +9,13 @@ from .crc32c import (  # noqa: F401
     Crc32cError,
     Crc32cLayer,
     append_csr,
+    append_host,
     batch_csr,
     batch_fixed,
     batch_host,
     batch_host_multi,
     dispatch,
+    egress_send_batch,
     filter_dispatch,
     xor_layer,
     xor_layer_csr,

@@ -71,6 +71,11 @@ def lib() -> ctypes.CDLL:
     L.lnl_ingress_recv_batch.restype = ctypes.c_int
     L.lnl_ingress_recv_batch.argtypes = [ctypes.c_int, _c_u8p, ctypes.c_size_t, _c_u8p, ctypes.c_uint32,
                                          ctypes.c_void_p, ctypes.c_int]
+    L.lnl_crc32c_append_host.restype = ctypes.c_int
+    L.lnl_crc32c_append_host.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, ctypes.c_int]
+    L.lnl_egress_send_batch.restype = ctypes.c_int64
+    L.lnl_egress_send_batch.argtypes = [ctypes.c_int, _c_u8p, _c_u8p, ctypes.c_uint32, ctypes.c_void_p,
+                                        ctypes.c_uint32, _c_u8p, ctypes.c_int]
     L.lnl_dispatch_csr_dev.restype = ctypes.c_int
     L.lnl_dispatch_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, _c_u8p, _c_u8p,
                                        ctypes.c_uint32, _c_u8p, ctypes.c_void_p]

@@ -394,6 +394,55 @@ def ingress_recv_batch(fd: int, buf: np.ndarray, max_n: int, wait_ms: int = 0):
     return r, off[: r + 1]
 
 
+def append_host(data: np.ndarray, offsets: np.ndarray, device: int = 0, want_crc: bool = False):
+    """Host-resident outbound layer over the GPU (H2D -> CRC + append -> D2H on
+    2 streams).  Blocking.  Returns (wire, wire_offsets[, crc]): datagram i is
+    wire[wire_offsets[i] .. wire_offsets[i + 1]) = payload || LE32(CRC), the
+    bytes Crc32cLayer.process_outbound gives for it.  Mirrors
+    lnl_crc32c_append_host."""
+    data, offsets = _host_csr(data, offsets)
+    n = offsets.size - 1
+    wire_off = (offsets - offsets[0]) + EXTRA_PACKET_SIZE * np.arange(n + 1, dtype=np.uint64)
+    wire = np.empty(int(wire_off[-1]), dtype=np.uint8)
+    crc = np.empty(max(n, 0), dtype=np.uint32) if want_crc else None
+    if n > 0:
+        check(lib().lnl_crc32c_append_host(data.ctypes.data, offsets.ctypes.data, n, wire.ctypes.data,
+                                           None if crc is None else crc.ctypes.data, device),
+              "lnl_crc32c_append_host")
+    return (wire, wire_off, crc) if want_crc else (wire, wire_off)
+
+
+def egress_send_batch(fd: int, wire: np.ndarray, offsets: np.ndarray, addrs=None, wait_ms: int = -1):
+    """One sendmmsg burst (in calls of <= 1024) of the CSR wire burst to UDP
+    socket fd.  addrs: None (connected socket), one (host, port) pair, or one
+    per datagram.  Returns (attempted, status): status[i] = bytes sent or a
+    negative errno for datagrams the kernel refused.  Mirrors
+    lnl_egress_send_batch."""
+    import socket
+    import struct
+    wire, offsets = _host_csr(wire, offsets)
+    n = offsets.size - 1
+    if n > 0 and int(offsets[0]) != 0:
+        raise ValueError("wire offsets must start at 0")
+    packed, naddrs = None, 0
+    if addrs is not None:
+        pairs = [addrs] if isinstance(addrs, tuple) else list(addrs)
+        if len(pairs) not in (1, n):
+            raise ValueError("addrs: one endpoint, or one per datagram")
+        # struct sockaddr_in: family (host order), port and address (network order), 8 pad bytes
+        raw = b"".join(struct.pack("=H", socket.AF_INET) + struct.pack("!H", p) + socket.inet_aton(h) + bytes(8)
+                       for h, p in pairs)
+        packed = np.frombuffer(raw, dtype=np.uint8).copy()
+        naddrs = len(pairs)
+    status = np.zeros(max(n, 0), dtype=np.int64)
+    r = lib().lnl_egress_send_batch(fd, wire.ctypes.data, offsets.ctypes.data, n,
+                                    None if packed is None else packed.ctypes.data, naddrs,
+                                    status.ctypes.data, wait_ms)
+    if r < 0:
+        raise Crc32cError(int(r), "lnl_egress_send_batch", os.strerror(int(-r)))
+    return int(r), status
+
+
 def batch_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
     """Host-resident batch over the GPU (H2D -> kernel -> D2H on 2 streams).
     Blocking.  ``data`` uint8, ``offsets`` uint64/int64 with n+1 entries."""

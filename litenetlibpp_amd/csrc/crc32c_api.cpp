@@ -68,7 +68,8 @@ struct DeviceState {
     uint8_t* d_bytes[2] = {nullptr, nullptr};
     uint64_t* d_off[2] = {nullptr, nullptr};
     uint32_t* d_out[2] = {nullptr, nullptr};
-    size_t cap_bytes = 0, cap_n = 0;
+    uint8_t* d_wire[2] = {nullptr, nullptr};  // append: the chunk's wire burst
+    size_t cap_bytes = 0, cap_n = 0, cap_wire = 0;
 };
 
 DeviceState g_dev[kMaxDevices];
@@ -504,6 +505,22 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
                uint32_t filter, void* hip_stream);
 }  // namespace
 
+namespace {
+// The outbound layer over a device burst whose CRCs go to crc (n words): the
+// CSR CRC pass, then the append kernel (lnl_append.hip).
+int append_csr(const DeviceState& S, const lnl::BatchArgs& src, uint8_t* d_dst, uint32_t* crc, hipStream_t st) {
+    lnl::BatchArgs a = src;
+    a.out = crc;
+    int rc = launch_csr(S, a, lnl::kModeCsr, st);
+    if (rc == 0) {
+        lnl::AppendArgs p{a.base, a.off, a.n, d_dst, crc, a.off0};
+        hipError_t e = lnl::launch_append(p, S.cus, st);
+        if (e != hipSuccess) rc = hip_fail(e, "append kernel launch");
+    }
+    return rc;
+}
+}  // namespace
+
 // The outbound layer over a device burst: the CSR CRC pass (into d_crc, or
 // stream-ordered scratch), then the append kernel (lnl_append.hip).
 extern "C" int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t* d_dst,
@@ -523,13 +540,7 @@ extern "C" int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* 
     a.base = d_base;
     a.off = d_off;
     a.n = n;
-    a.out = crc;
-    int rc = launch_csr(*S, a, lnl::kModeCsr, st);
-    if (rc == 0) {
-        lnl::AppendArgs p{d_base, d_off, n, d_dst, crc};
-        hipError_t e = lnl::launch_append(p, S->cus, st);
-        if (e != hipSuccess) rc = hip_fail(e, "append kernel launch");
-    }
+    int rc = append_csr(*S, a, d_dst, crc, st);
     if (!d_crc) {
         hipError_t e = hipFreeAsync(crc, st);
         if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
@@ -609,13 +620,18 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
 // D2H (CRCs).  Stream order makes buffer reuse safe; the two streams overlap
 // one chunk's copies with the other's kernel.
 namespace {
-// Host-resident CSR batch through `device` (lnl_crc32c_batch_host and
-// lnl_inbound_filter_host): chunks over two streams, H2D -> kernel -> D2H.
-// filter = 0: h_out is u32 CRCs; 1: h_out is u8 inbound status codes.
+// Host-resident CSR batch through `device` (lnl_crc32c_batch_host,
+// lnl_inbound_filter_host, lnl_crc32c_append_host): chunks over two streams,
+// H2D -> kernel -> D2H.
+enum HostMode : uint32_t { kHostCrc = 0, kHostFilter = 1, kHostAppend = 2 };
+// kHostCrc: h_out is u32 CRCs; kHostFilter: u8 inbound status codes;
+// kHostAppend: h_out is the wire burst (payload || LE32(CRC) per datagram,
+// back to back) and h_crc (optional) the CRCs
 int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h_out, int device,
-               uint32_t filter) {
+               uint32_t mode, uint32_t* h_crc = nullptr) {
     if (n == 0) return 0;
     if (!h_base || !h_off || !h_out) return fail(-EINVAL, "NULL argument");
+    const uint32_t filter = mode == kHostFilter;
     for (uint32_t i = 0; i < n; ++i)
         if (h_off[i + 1] < h_off[i]) return fail(-EINVAL, "offsets decrease at %u", i);
     DeviceState* S;
@@ -656,11 +672,13 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
             (void)hipFree(S->d_bytes[k]);
             (void)hipFree(S->d_off[k]);
             (void)hipFree(S->d_out[k]);
+            (void)hipFree(S->d_wire[k]);
             S->d_bytes[k] = nullptr;
             S->d_off[k] = nullptr;
             S->d_out[k] = nullptr;
+            S->d_wire[k] = nullptr;
         }
-        S->cap_bytes = S->cap_n = 0;
+        S->cap_bytes = S->cap_n = S->cap_wire = 0;
         const size_t nb = std::max<size_t>(need_bytes, 256);
         for (int k = 0; k < 2; ++k) {
             if ((e = hipMalloc(&S->d_bytes[k], nb)) != hipSuccess ||
@@ -670,6 +688,18 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         }
         S->cap_bytes = nb;
         S->cap_n = need_n;
+    }
+    const size_t need_wire = S->cap_bytes + (size_t)S->cap_n * LNL_CRC32C_LAYER_EXTRA;
+    if (mode == kHostAppend && need_wire > S->cap_wire) {  // the wire staging, on the first append only
+        for (int k = 0; k < 2; ++k) {
+            (void)hipFree(S->d_wire[k]);
+            S->d_wire[k] = nullptr;
+        }
+        S->cap_wire = 0;
+        for (int k = 0; k < 2; ++k)
+            if ((e = hipMalloc(&S->d_wire[k], need_wire)) != hipSuccess)
+                return fail(-ENOMEM, "wire staging allocation: %s", hipGetErrorString(e));
+        S->cap_wire = need_wire;
     }
     // after the first enqueue, every error path drains both streams first: the
     // caller may free h_base / h_out as soon as we return
@@ -697,6 +727,21 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         a.off0 = h_off[i];
         a.n = cn;
         const size_t esz = filter ? 1 : 4;  // bytes of output per datagram
+        if (mode == kHostAppend) {
+            // the chunk's wire burst starts where its first datagram's wire
+            // bytes go: (h_off[i] - h_off[0]) + 4 i
+            if (int rc = append_csr(*S, a, S->d_wire[k], S->d_out[k], st)) return drained(rc);
+            uint8_t* dst = (uint8_t*)h_out + (h_off[i] - h_off[0]) + (size_t)i * LNL_CRC32C_LAYER_EXTRA;
+            if ((e = hipMemcpyAsync(dst, S->d_wire[k], cb + (size_t)cn * LNL_CRC32C_LAYER_EXTRA,
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return drained(hip_fail(e, "D2H wire"));
+            if (h_crc && (e = hipMemcpyAsync(h_crc + i, S->d_out[k], (size_t)cn * 4, hipMemcpyDeviceToHost, st)) !=
+                             hipSuccess)
+                return drained(hip_fail(e, "D2H crc"));
+            i = j;
+            k ^= 1;
+            continue;
+        }
         if (filter) {
             a.ok = (uint8_t*)S->d_out[k];
             a.filter = 1;
@@ -719,12 +764,17 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
 
 extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                                      uint32_t* h_out, int device) {
-    return host_batch(h_base, h_off, n, h_out, device, 0u);
+    return host_batch(h_base, h_off, n, h_out, device, kHostCrc);
 }
 
 extern "C" int lnl_inbound_filter_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                                        uint8_t* h_status, int device) {
-    return host_batch(h_base, h_off, n, h_status, device, 1u);
+    return host_batch(h_base, h_off, n, h_status, device, kHostFilter);
+}
+
+extern "C" int lnl_crc32c_append_host(const uint8_t* h_payload, const uint64_t* h_off, uint32_t n, uint8_t* h_wire,
+                                      uint32_t* h_crc, int device) {
+    return host_batch(h_payload, h_off, n, h_wire, device, kHostAppend, h_crc);
 }
 
 extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,

@@ -206,6 +206,7 @@ struct AppendArgs {
     uint32_t n;
     uint8_t* dst;
     const uint32_t* crc;
+    uint64_t off0;  // datagram i's bytes are base[off[i] - off0 ..) (host-path chunks: off0 = off[0])
 };
 hipError_t launch_append(const AppendArgs& a, int cus, hipStream_t stream);
 

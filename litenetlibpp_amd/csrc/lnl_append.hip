@@ -46,7 +46,7 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
     const uint32_t nt = gridDim.x * (kThreads / kTeam);
     const uint32_t q = threadIdx.x % kTeam;  // lane within the team
     const uint64_t o0 = a.off[0];
-    const uint64_t dstb = (uint64_t)(uintptr_t)a.dst, srcb = (uint64_t)(uintptr_t)a.base;
+    const uint64_t dstb = (uint64_t)(uintptr_t)a.dst, srcb = (uint64_t)(uintptr_t)a.base - a.off0;
     // the next datagram's offsets and CRC are fetched one datagram ahead
     uint64_t ns = 0, ne = 0;
     uint32_t ncrc = 0;

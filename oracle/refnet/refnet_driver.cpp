@@ -22,6 +22,14 @@
 //                               variant: the reference's own loss handling)
 //   refnet_driver bench         1000 x 256 B echoes, UNRELIABLE and
 //                               RELIABLE_ORDERED
+//   refnet_driver merged IN OUT crafted MERGED containers (file IN, written by
+//                               tests/golden/make_dispatch_ref.py) sent one by
+//                               one from the client's own endpoint (the wrapper
+//                               replaces one outgoing datagram, refnet_inject):
+//                               the server's net_peer::process_packet cuts them
+//                               (net_peer.cpp:164-187); every packet it
+//                               delivers to the listener (method, payload) is
+//                               written to OUT as JSON, per container
 //
 // Each mode prints one JSON line and exits 0 when its checks pass.
 #include <lnl/lnl.h>
@@ -49,6 +57,8 @@ void refnet_reset_max_sent(void);
 void refnet_set_flip_every(uint32_t n);
 void refnet_set_lose_every(uint32_t n);
 uint64_t refnet_lost(void);
+void refnet_inject(const uint8_t* p, size_t n, uint16_t port_be);
+uint64_t refnet_injected(void);
 }
 
 namespace {
@@ -359,6 +369,84 @@ int t_bench() {
     return finish(ok, js);
 }
 
+// ---- MERGED containers through the reference's process_packet ------------------
+// Input: "LNLM", u32 count, u32 connection number, then per container u32 length
+// + bytes (header byte first, no CRC field: the layer adds it on the way).  Each
+// one replaces the client's next datagram to the server (a TRIG message makes
+// one); a MARK message sent after it closes the container's deliveries (UDP
+// loopback and the server's single receive thread keep the order).
+int t_merged(const char* in_path, const char* out_path) {
+    FILE* f = fopen(in_path, "rb");
+    if (!f) return finish(false, "\"test\": \"merged\", \"stage\": \"open input\"");
+    char magic[4];
+    uint32_t count = 0, conn = 0;
+    bool ok = fread(magic, 1, 4, f) == 4 && memcmp(magic, "LNLM", 4) == 0 && fread(&count, 4, 1, f) == 1 &&
+              fread(&conn, 4, 1, f) == 1;
+    std::vector<std::vector<uint8_t>> cont(ok ? count : 0);
+    for (auto& c : cont) {
+        uint32_t n = 0;
+        ok = ok && fread(&n, 4, 1, f) == 1 && n <= 65507;
+        c.resize(ok ? n : 0);
+        ok = ok && fread(c.data(), 1, c.size(), f) == c.size();
+    }
+    fclose(f);
+    if (!ok) return finish(false, "\"test\": \"merged\", \"stage\": \"read input\"");
+    Pair P;
+    static const uint8_t kTrig[4] = {'T', 'R', 'I', 'G'}, kMark[4] = {'M', 'A', 'R', 'K'};
+    std::vector<std::pair<int, std::vector<uint8_t>>> got;  // (method, payload)
+    int marks = 0;
+    P.sl.network_receive().subscribe([&](auto&, lnl::net_data_reader& reader, auto, auto method) {
+        std::vector<uint8_t> b(reader.remaining());
+        if (!b.empty() && !reader.try_read(b.data(), b.size())) return;
+        if (b.size() == 8 && memcmp(b.data(), kMark, 4) == 0) {
+            ++marks;
+            return;
+        }
+        if (b.size() == 4 && memcmp(b.data(), kTrig, 4) == 0) return;  // a trigger the injection did not replace
+        got.emplace_back((int)method, std::move(b));
+    });
+    if (!P.connect()) return finish(false, "\"test\": \"merged\", \"stage\": \"connect\"");
+    const auto server_peer = P.server.first_peer();
+    if (!server_peer || server_peer->connect_number() != conn || P.client_peer->connect_number() != conn) {
+        char b[160];
+        snprintf(b, sizeof b, "\"test\": \"merged\", \"stage\": \"connection number\", \"expected\": %u", conn);
+        return finish(false, b);
+    }
+    lnl::net_address sa(P.server.address());
+    const uint16_t port_be = sa.raw.sin_port;
+    FILE* o = fopen(out_path, "w");
+    if (!o) return finish(false, "\"test\": \"merged\", \"stage\": \"open output\"");
+    fprintf(o, "{\"containers\": %u, \"connection_number\": %u, \"delivered\": [\n", count, conn);
+    const std::vector<uint8_t> trig(kTrig, kTrig + 4);
+    uint32_t done_ok = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        got.clear();
+        const uint64_t before = refnet_injected();
+        refnet_inject(cont[i].data(), cont[i].size(), port_be);
+        P.client_peer->send(trig, lnl::DELIVERY_METHOD::UNRELIABLE);
+        bool sent = pump(P.client, P.server, 3.0, [&] { return refnet_injected() > before; }, 200);
+        const int want = marks + 1;
+        std::vector<uint8_t> mark(kMark, kMark + 4);
+        for (int k = 0; k < 4; ++k) mark.push_back((uint8_t)(i >> (8 * k)));
+        P.client_peer->send(mark, lnl::DELIVERY_METHOD::UNRELIABLE);
+        bool closed = sent && pump(P.client, P.server, 3.0, [&] { return marks >= want; }, 200);
+        if (!closed) break;
+        ++done_ok;
+        fprintf(o, "%s[", i ? ",\n" : "");
+        for (size_t k = 0; k < got.size(); ++k) {
+            fprintf(o, "%s[%d, \"", k ? ", " : "", got[k].first);
+            for (uint8_t v : got[k].second) fprintf(o, "%02x", v);
+            fprintf(o, "\"]");
+        }
+        fprintf(o, "]");
+    }
+    fprintf(o, "\n]}\n");
+    fclose(o);
+    char b[160];
+    snprintf(b, sizeof b, "\"test\": \"merged\", \"containers\": %u, \"closed\": %u", count, done_ok);
+    return finish(done_ok == count, b);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -371,6 +459,7 @@ int main(int argc, char** argv) {
     if (mode == "flip") return t_flip(argc > 2 ? (uint32_t)atoi(argv[2]) : 5u, false);
     if (mode == "lose") return t_flip(argc > 2 ? (uint32_t)atoi(argv[2]) : 5u, true);
     if (mode == "bench") return t_bench();
-    fprintf(stderr, "usage: %s connect|send_receive|echo|mtu|flip [n]|bench\n", argv[0]);
+    if (mode == "merged" && argc > 3) return t_merged(argv[2], argv[3]);
+    fprintf(stderr, "usage: %s connect|send_receive|echo|mtu|flip [n]|bench|merged IN OUT\n", argv[0]);
     return 2;
 }

@@ -24,14 +24,21 @@
 // largest datagram it put on the wire, which is how the tests read the MTU the
 // probe settled on (net_peer keeps m_mtu private).  refnet_set_flip_every(n)
 // corrupts one bit of every n-th outgoing datagram after the CRC was written:
-// a bit-flipping link.
+// a bit-flipping link.  refnet_inject(bytes, port) replaces the next datagram
+// sent to that (network-order) port with the given bytes, before the layer:
+// crafted datagrams then reach the other manager from a connected peer's own
+// endpoint (the MERGED-cut fixture, refnet_driver merged).
 #include <errno.h>
 #include <stdint.h>
 #include <string.h>
 #include <sys/socket.h>
 #include <sys/types.h>
 
+#include <netinet/in.h>
+
 #include <atomic>
+#include <mutex>
+#include <vector>
 
 #include "../../include/lnl_crc32c.h"
 
@@ -60,6 +67,23 @@ bool lose() {
     return true;
 }
 
+// one pending injection: bytes and the destination port it replaces a datagram to
+std::mutex g_inj_mu;
+std::vector<uint8_t> g_inj;
+bool g_inj_pending = false;
+uint16_t g_inj_port = 0;
+std::atomic<uint64_t> g_inj_done{0};
+
+// the datagram to send instead of buf, or null (keeps buf)
+bool take_injection(const struct sockaddr* addr, socklen_t alen, std::vector<uint8_t>& out) {
+    if (!addr || alen < (socklen_t)sizeof(sockaddr_in) || addr->sa_family != AF_INET) return false;
+    std::lock_guard<std::mutex> lk(g_inj_mu);
+    if (!g_inj_pending || ((const sockaddr_in*)addr)->sin_port != g_inj_port) return false;
+    out.swap(g_inj);
+    g_inj_pending = false;
+    return true;
+}
+
 void note_sent(int64_t n) {
     g_sent.fetch_add(1, std::memory_order_relaxed);
     int64_t m = g_max_sent.load(std::memory_order_relaxed);
@@ -71,6 +95,19 @@ void note_sent(int64_t n) {
 extern "C" {
 
 ssize_t __wrap_sendto(int fd, const void* buf, size_t len, int flags, const struct sockaddr* addr, socklen_t alen) {
+    thread_local std::vector<uint8_t> inj;
+    const size_t caller_len = len;
+    const bool injected = take_injection(addr, alen, inj);
+    if (injected) {
+        buf = inj.data();
+        len = inj.size();
+    }
+    struct Done {  // count the injection once it has gone out (or was lost)
+        bool on;
+        ~Done() {
+            if (on) g_inj_done.fetch_add(1);
+        }
+    } done{injected};
 #if REFNET_CRC
     thread_local uint8_t scratch[65536 + LNL_CRC32C_LAYER_EXTRA];
     const int64_t wire = lnl_crc32c_layer_outbound((const uint8_t*)buf, 0, len, scratch, sizeof scratch);
@@ -89,11 +126,13 @@ ssize_t __wrap_sendto(int fd, const void* buf, size_t len, int flags, const stru
     }
     note_sent(wire);
     if (lose()) return wire;
-    return __real_sendto(fd, scratch, (size_t)wire, flags, addr, alen);
+    const ssize_t r = __real_sendto(fd, scratch, (size_t)wire, flags, addr, alen);
+    return injected && r >= 0 ? (ssize_t)caller_len : r;
 #else
     note_sent((int64_t)len);
     if (lose()) return (ssize_t)len;
-    return __real_sendto(fd, buf, len, flags, addr, alen);
+    const ssize_t r = __real_sendto(fd, buf, len, flags, addr, alen);
+    return injected && r >= 0 ? (ssize_t)caller_len : r;
 #endif
 }
 
@@ -129,5 +168,12 @@ void refnet_reset_max_sent(void) { g_max_sent.store(0); }
 void refnet_set_flip_every(uint32_t n) { g_flip_every.store(n); }
 void refnet_set_lose_every(uint32_t n) { g_lose_every.store(n); }
 uint64_t refnet_lost(void) { return g_lost.load(); }
+void refnet_inject(const uint8_t* p, size_t n, uint16_t port_be) {
+    std::lock_guard<std::mutex> lk(g_inj_mu);
+    g_inj.assign(p, p + n);
+    g_inj_port = port_be;
+    g_inj_pending = true;
+}
+uint64_t refnet_injected(void) { return g_inj_done.load(); }
 
 }  // extern "C"

@@ -165,6 +165,41 @@ def dispatch(wire_list, status):
     return out
 
 
+def cut_merged(pkt):
+    """The entries of one MERGED packet under dispatch()'s rules (bounded by the
+    packet itself): [(offset, length)]."""
+    out, pos, size = [], 1, len(pkt)
+    while pos + 2 <= size:
+        L = int(pkt[pos]) | (int(pkt[pos + 1]) << 8)
+        pos += 2
+        if L > size - pos or L == 0 or not packet_verify(int(pkt[pos]), L):
+            break
+        out.append((pos, L))
+        pos += L
+    return out
+
+
+def deliver(pkt, conn):
+    """What net_peer::process_packet hands the user for one dispatched packet
+    (/root/reference/src/lnl/net_peer.cpp:138-243), for the properties the
+    dispatch fixture uses: dropped unless its connection number is conn (:156);
+    UNRELIABLE -> [payload after the 1-byte header] (:240-243); MERGED -> its
+    entries (cut_merged: the product's datagram-bounded rule), each delivered
+    the same way; anything else -> nothing."""
+    pkt = bytes(pkt)
+    if not pkt or ((pkt[0] & 0x60) >> 5) != conn:
+        return []
+    prop = pkt[0] & 0x1F
+    if prop == 0:
+        return [pkt[1:]]
+    if prop != MERGED_PROPERTY:
+        return []
+    out = []
+    for o, L in cut_merged(pkt):
+        out += deliver(pkt[o:o + L], conn)
+    return out
+
+
 def xor_layer(data: np.ndarray, key: bytes) -> np.ndarray:
     """Upstream LiteNetLib XorEncryptLayer on one datagram (restated; the C#
     source is not available offline -- parity unpinned):

@@ -37,7 +37,8 @@ def test_header_declares_the_boundary():
               "lnl_crc32c_layer_outbound", "lnl_crc32c_layer_inbound", "lnl_crc32c_last_error",
               "lnl_crc32c_batch_host_multi", "lnl_packet_verify", "lnl_inbound_status",
               "lnl_inbound_filter_csr_dev", "lnl_inbound_filter_host", "lnl_ingress_recv_batch",
-              "lnl_dispatch_csr_dev", "lnl_inbound_filter_dispatch_csr_dev", "lnl_xor_layer", "lnl_xor_layer_csr_dev", "lnl_xor_layer_fixed_dev"):
+              "lnl_dispatch_csr_dev", "lnl_inbound_filter_dispatch_csr_dev", "lnl_xor_layer", "lnl_xor_layer_csr_dev", "lnl_xor_layer_fixed_dev",
+              "lnl_crc32c_append_host", "lnl_egress_send_batch"):
         assert s in syms
 
 
@@ -47,7 +48,7 @@ def test_library_exports_every_declared_symbol(pkg):
     exported = set(re.findall(r"\bT (lnl_\w+)", out))
     missing = [s for s in declared_symbols() if s not in exported]
     assert not missing, missing
-    assert pkg.lib().lnl_crc32c_abi_version() == 7
+    assert pkg.lib().lnl_crc32c_abi_version() == 8
 
 
 def test_ctypes_bindings_match_the_header(pkg):
@@ -136,6 +137,11 @@ def test_batch_entry_points_refuse_without_gpu(pkg):
                                                None, None, None, 0, ctypes.addressof(tot), None)
     assert rc == -19, rc
     assert list(st) == [0, 0, 0, 0] and tot[0] == 7
+    # the host outbound layer: no device, no wire bytes
+    wire = (ctypes.c_uint8 * 80)()
+    rc = L.lnl_crc32c_append_host(ctypes.addressof(buf), ctypes.addressof(off), 4, ctypes.addressof(wire), None, 0)
+    assert rc == -19, rc
+    assert bytes(wire) == bytes(80)
 
 
 def test_product_library_has_no_experiment_knobs(pkg):
@@ -163,6 +169,7 @@ def test_host_batch_offsets_checked_before_the_call(pkg):
     for off in (np.array([0, 50, 101], np.uint64), np.array([0, 60, 50], np.int64),
                 np.array([-8, 10], np.int64)):
         for fn in (lambda o: pkg.batch_host(data, o, 0), lambda o: pkg.inbound_filter_host(data, o, 0),
-                   lambda o: pkg.batch_host_multi(data, o, [0])):
+                   lambda o: pkg.batch_host_multi(data, o, [0]), lambda o: pkg.append_host(data, o, 0),
+                   lambda o: pkg.egress_send_batch(0, data, o)):
             with pytest.raises(ValueError):
                 fn(off)

@@ -44,6 +44,18 @@ def test_gpus_8_names_config4():
     assert line["config"]["workload"].startswith("config4")
 
 
+def test_dead_rank_ends_the_run():
+    """A rank that dies before rendezvous: the spawner stops its siblings (which
+    would wait for it forever) and returns the dead rank's status."""
+    import time
+    t0 = time.time()
+    r = _run(["--gpus", "4", "--steps", "2", "--warmup", "0", "--packets", "64"],
+             extra_env={"LNL_BENCH_DRYRUN_FAIL_RANK": "2"}, timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "rank 2 exited with status 3" in r.stderr
+    assert time.time() - t0 < 90
+
+
 def test_world_size_mismatch_is_refused():
     r = _run(["--gpus", "2", "--steps", "1"], extra_env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0

@@ -444,22 +444,26 @@ def test_host_multi_device_path(P, devices):
     assert np.array_equal(got, oracle.batch_csr(data, off))
 
 
-@pytest.mark.parametrize("receivers", [1, 3])
-def test_socket_example_receivers(P, receivers):
+@pytest.mark.parametrize("receivers,egress", [(1, 0), (3, 0), (1, 1), (2, 1)])
+def test_socket_example_receivers(P, receivers, egress):
     """examples/socket_path (built by build()): R SO_REUSEPORT receive sockets,
     one thread and pinned burst buffer each, GPU filter per burst; every GPU
-    status equals lnl_inbound_status on the CPU (exit code 3 otherwise)."""
+    status equals lnl_inbound_status on the CPU (exit code 3 otherwise).  With
+    --egress 1 the senders run the product's send side per burst
+    (lnl_crc32c_append_host, then lnl_egress_send_batch)."""
     import json
     import subprocess
     exe = os.path.join(ROOT, "examples", "socket_path")
     if not os.path.exists(exe):
         pytest.fail("examples/socket_path not built (run __graft_entry__.build())")
-    r = subprocess.run([exe, "--count", "30000", "--burst", "1024", "--receivers", str(receivers)],
-                       capture_output=True, text=True, timeout=90)
+    r = subprocess.run([exe, "--count", "30000", "--burst", "1024", "--receivers", str(receivers),
+                        "--egress", str(egress)], capture_output=True, text=True, timeout=90)
     assert r.returncode == 0, r.stderr
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["gpu_cpu_mismatch"] == 0 and j["receivers"] == receivers
     assert j["received"] >= 0.5 * j["sent"] and j["accept"] > 0 and j["drop_crc"] > 0
+    if egress:
+        assert j["egress"] and j["tx_payload_bytes"] > 0 and j["append_host_gbps"] > 0
 
 
 def test_socket_path_end_to_end(P):
@@ -498,6 +502,110 @@ def test_socket_path_end_to_end(P):
     assert got_wire == sent
     exp = [oracle.inbound_status(np.frombuffer(w, np.uint8)) for w in sent]
     assert got_status == exp and set(exp) == {0, 1, 2}
+
+
+@pytest.mark.parametrize("n,shift", [(1, 0), (777, 3), (200_000, 11)])
+def test_append_host_matches_layer_outbound(P, n, shift):
+    """lnl_crc32c_append_host (pinned payload burst -> H2D -> CRC + append ->
+    D2H, chunks over 2 streams; 200,000 datagrams take several chunks): every
+    wire byte equals lnl_crc32c_layer_outbound of its payload, back to back, and
+    the CRCs equal the oracle's.  Nonzero first offset."""
+    rng = np.random.default_rng(400 + n)
+    lens = rng.integers(0, 1429, n)
+    lens[: min(n, 4)] = [0, 1, 1428, 64][: min(n, 4)]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(shift)
+    data = rng.integers(0, 256, int(off[-1]) + 7, dtype=np.uint8)
+    pinned = torch.from_numpy(data).pin_memory().numpy()
+    wire, woff, crc = P.append_host(pinned, off, 0, want_crc=True)
+    exp = oracle.batch_csr(data, off)
+    assert np.array_equal(crc, exp)
+    assert wire.size == int(off[-1] - off[0]) + 4 * n
+    assert np.array_equal(np.diff(woff.astype(np.int64)), lens + 4)
+    crcpos = woff[1:].astype(np.int64) - 4
+    keep = np.ones(wire.size, dtype=bool)
+    for j in range(4):
+        keep[crcpos + j] = False
+    assert np.array_equal(wire[keep], data[int(off[0]):int(off[-1])])
+    assert np.array_equal(wire[crcpos[:, None] + np.arange(4)[None, :]].reshape(-1), exp.astype("<u4").view(np.uint8))
+    layer = P.Crc32cLayer()
+    for i in list(range(min(n, 50))) + [n - 1]:
+        w = bytes(wire[int(woff[i]):int(woff[i + 1])])
+        assert w == layer.process_outbound(data[int(off[i]):int(off[i + 1])].tobytes())
+
+
+def test_append_host_egress_loopback(P):
+    """The send half of the socket path end to end:
+    payload bursts in pinned memory -> lnl_crc32c_append_host -> one
+    lnl_egress_send_batch (sendmmsg) per burst over UDP loopback ->
+    lnl_ingress_recv_batch on the receiver.  Every received datagram equals
+    lnl_crc32c_layer_outbound of its payload and passes lnl_inbound_status (and
+    the GPU filter)."""
+    import socket
+    rng = np.random.default_rng(808)
+    rx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 23)
+    rx.bind(("127.0.0.1", 0))
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    layer = P.Crc32cLayer()
+    burst, bursts = 48, 25
+    rbuf = torch.empty(burst * P.INGRESS_SLOT, dtype=torch.uint8).pin_memory().numpy()
+    sent_payloads, got = [], []
+    for b in range(bursts):
+        lens = rng.integers(16, 1429, burst)  # >= every header the chosen bytes need
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        data = torch.from_numpy(rng.integers(0, 256, int(off[-1]), dtype=np.uint8)).pin_memory().numpy()
+        data[off[:-1].astype(np.int64)] = rng.choice([0x00, 0x01, 0x81], burst)  # header bytes verify() accepts
+        wire, woff = P.append_host(data, off, 0)
+        r, st = P.egress_send_batch(tx.fileno(), wire, woff, addrs=rx.getsockname())
+        assert r == burst and bool((st == lens + 4).all())
+        sent_payloads += [data[int(off[i]):int(off[i + 1])].tobytes() for i in range(burst)]
+        k = 0
+        while k < burst:
+            n, roff = P.ingress_recv_batch(rx.fileno(), rbuf, burst, wait_ms=2000)
+            assert n > 0, f"timed out in burst {b} after {k}"
+            st_gpu = P.inbound_filter_host(rbuf, roff, 0)
+            assert bool((st_gpu == P.INBOUND_ACCEPT).all())
+            got += [bytes(rbuf[int(roff[i]):int(roff[i + 1])]) for i in range(n)]
+            k += n
+    rx.close()
+    tx.close()
+    assert len(got) == len(sent_payloads)
+    for p, w in zip(sent_payloads, got):
+        assert w == layer.process_outbound(p)
+        assert P.inbound_status(w) == P.INBOUND_ACCEPT
+
+
+@pytest.mark.parametrize("replicas,fused", [(1, False), (1, True), (150, False), (150, True)])
+def test_dispatch_reference_fixture(P, replicas, fused):
+    """The MERGED cut against the REFERENCE's own process_packet
+    (tests/golden/dispatch_ref.*, made by running the reference's net_manager:
+    tests/golden/make_dispatch_ref.py): every container of the fixture, as a
+    wire datagram with its CRC, through lnl_inbound_filter_csr_dev +
+    lnl_dispatch_csr_dev or the fused lnl_inbound_filter_dispatch_csr_dev;
+    the packets each container gives, handed to the caller's process_packet
+    (oracle.deliver), must be exactly what the reference delivered -- or, where
+    the reference reads past the datagram, exactly the deliveries before that
+    read.  150 replicas (17,250 datagrams, shuffled) take the span path."""
+    from test_dispatch_ref import expected, load_fixture, with_crc
+    cont, conn, recs = load_fixture()
+    rng = np.random.default_rng(60 + replicas)
+    order = np.concatenate([rng.permutation(len(cont)) for _ in range(replicas)])
+    wires = [with_crc(cont[k]) for k in order]
+    lead = int(rng.integers(0, 64))
+    off = np.concatenate([[0], np.cumsum([len(w) for w in wires])]).astype(np.uint64) + np.uint64(lead)
+    data = np.frombuffer(bytes(lead) + b"".join(wires) + bytes(5), dtype=np.uint8)
+    d, o = dev(data), dev(off.view(np.int64), torch.int64)
+    if fused:
+        status, start, length, parent = P.filter_dispatch(d, o)
+    else:
+        status = P.inbound_filter(d, o)
+        start, length, parent = P.dispatch(d, o, status)
+    assert bool((status == P.INBOUND_ACCEPT).all())
+    got = [[] for _ in wires]
+    for s0, L, i in zip(start.cpu().numpy(), length.cpu().numpy(), parent.cpu().numpy()):
+        got[int(i)] += oracle.deliver(data[int(s0):int(s0) + int(L)], conn)
+    bad = [j for j, k in enumerate(order) if got[j] != expected(recs[k])]
+    assert not bad, [(j, int(order[j])) for j in bad[:8]]
 
 
 def _merged(rng, parts, mode):
