@@ -414,6 +414,28 @@ def host_path_rate(P, host, w, device):
                     f"mean of {reps} calls"}, got
 
 
+def host_append_rate(P, host, w, device):
+    """The send side from host memory: the same payload burst, pinned, through
+    lnl_crc32c_append_host (H2D + CRC + append + D2H of the wire burst, 2
+    streams), PCIe-inclusive; the wire bytes of the first datagrams checked
+    against the device-resident call's."""
+    data, off = host
+    pinned = torch.from_numpy(data).pin_memory().numpy()
+    wire, woff = P.append_host(pinned, off, device)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        P.append_host(pinned, off, device)
+    dt = (time.perf_counter() - t0) / reps
+    k = min(w["n"], 1 << 14)
+    ok = np.array_equal(wire[: int(woff[k])], w["wire"][: int(woff[k])].cpu().numpy())
+    return {"value": round(w["payload"] / dt / 1e9, 2), "unit": "GB/s",
+            "what": "the payload burst in pinned host memory through lnl_crc32c_append_host (H2D payload + "
+                    "offsets, CRC + append, D2H wire burst; 2 streams), blocking, payload bytes / time, "
+                    f"mean of {reps} calls",
+            "parity": "wire bytes equal the device-resident call's" if ok else "MISMATCH"}
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
@@ -626,6 +648,8 @@ def main():
                 "cpu_model": cpu_model(),
             }
             line["parity_whole_batch"] = "bit-exact" if exact else "MISMATCH"
+        if world == 1 and w.get("append") and not args.no_host_path:  # the send side from host memory
+            line["host_append"] = host_append_rate(P, host, w, torch.cuda.current_device())
         if world == 1 and crc_workload and not args.no_host_path:
             hp, got = host_path_rate(P, host, w, torch.cuda.current_device())
             hp["parity"] = "bit-exact vs the device-resident output" if np.array_equal(
