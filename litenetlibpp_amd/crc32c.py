@@ -394,16 +394,23 @@ def ingress_recv_batch(fd: int, buf: np.ndarray, max_n: int, wait_ms: int = 0):
     return r, off[: r + 1]
 
 
-def append_host(data: np.ndarray, offsets: np.ndarray, device: int = 0, want_crc: bool = False):
+def append_host(data: np.ndarray, offsets: np.ndarray, device: int = 0, want_crc: bool = False, out=None):
     """Host-resident outbound layer over the GPU (H2D -> CRC + append -> D2H on
     2 streams).  Blocking.  Returns (wire, wire_offsets[, crc]): datagram i is
     wire[wire_offsets[i] .. wire_offsets[i + 1]) = payload || LE32(CRC), the
-    bytes Crc32cLayer.process_outbound gives for it.  Mirrors
-    lnl_crc32c_append_host."""
+    bytes Crc32cLayer.process_outbound gives for it.  ``out``: a uint8 array of
+    at least the wire burst's size to write it into -- pinned memory (as for
+    ``data``) gives the full PCIe rate; a fresh pageable array otherwise.
+    Mirrors lnl_crc32c_append_host."""
     data, offsets = _host_csr(data, offsets)
     n = offsets.size - 1
     wire_off = (offsets - offsets[0]) + EXTRA_PACKET_SIZE * np.arange(n + 1, dtype=np.uint64)
-    wire = np.empty(int(wire_off[-1]), dtype=np.uint8)
+    if out is not None:
+        if out.dtype != np.uint8 or not out.flags["C_CONTIGUOUS"] or out.size < int(wire_off[-1]):
+            raise ValueError("out must be a contiguous uint8 array of at least the wire burst's size")
+        wire = out[: int(wire_off[-1])]
+    else:
+        wire = np.empty(int(wire_off[-1]), dtype=np.uint8)
     crc = np.empty(max(n, 0), dtype=np.uint32) if want_crc else None
     if n > 0:
         check(lib().lnl_crc32c_append_host(data.ctypes.data, offsets.ctypes.data, n, wire.ctypes.data,

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -326,14 +327,51 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 #ifndef LNL_SPAN_FIX_WGS
 #define LNL_SPAN_FIX_WGS 0xFFFFFFFFu  // cap on the batch kernel's grid after the span kernel (experiments)
 #endif
+// The span path's scratch is kept per (device, stream) across calls: its two
+// control blocks (crc32c_span.h kSpanCtlWords) are used by alternate calls and
+// each call's batch kernel zeroes the other one's overflow count, so no call
+// needs a memset or a pre-pass launch.  It grows stream-ordered (hipFreeAsync /
+// hipMallocAsync on the stream), and the blocks are zeroed once when it does.
+// g_span_mu is held from the parity's choice through the launches, so a
+// stream's calls take the blocks in launch order even from several threads.
+struct SpanScratch {
+    uint32_t* buf = nullptr;
+    size_t words = 0;
+    uint64_t calls = 0;
+};
+std::mutex g_span_mu;
+std::map<std::pair<int, hipStream_t>, SpanScratch> g_span_scratch;
+
+int span_scratch(hipStream_t st, size_t words, uint32_t** buf, uint32_t* parity) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    SpanScratch& s = g_span_scratch[{dev, st}];
+    if (s.words < words) {
+        const size_t grow = words + words / 4;  // headroom: batches of similar sizes reuse it
+        if (s.buf) (void)hipFreeAsync(s.buf, st);
+        s.buf = nullptr;
+        s.words = 0;
+        hipError_t e = hipMallocAsync((void**)&s.buf, grow * sizeof(uint32_t), st);
+        if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", grow * 4, hipGetErrorString(e));
+        e = hipMemsetAsync(s.buf, 0, 2 * lnl::kSpanCtlWords * sizeof(uint32_t), st);
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+        s.words = grow;
+        s.calls = 0;
+    }
+    *buf = s.buf;
+    *parity = (uint32_t)(s.calls++ & 1u);
+    return 0;
+}
+
 // CSR batches (product path): the span kernel (crc32c_span.hip: every line read
-// once, one 512-thread workgroup per CU) after its pre-pass, then the batch
-// kernel, which completes the cross-segment heads and takes the datagrams the
-// span kernel leaves (three or more segments; device-side count).
+// once, one 512-thread workgroup per CU; no pre-pass), then the batch kernel,
+// which completes the cross-wave-batch heads and takes the datagrams the span
+// kernel leaves (three or more segments; device-side count), or the whole batch
+// when the span kernel does not take it.
 // (span_mode: kSpanCrc -> out[i]; kSpanVerify / kSpanFilter -> ok[i], the
 // overflow datagrams through the batch kernel in verify mode)
 int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st, uint32_t span_mode = lnl::kSpanCrc,
-                    uint32_t* walk_blocks = nullptr) {
+                    uint32_t* walk_blocks = nullptr, const uint32_t** span_ctl = nullptr) {
     lnl::SpanArgs g{};
     g.mode = span_mode;
     g.wblk = walk_blocks;  // filter + dispatch: the MERGED walk in the same pass
@@ -345,27 +383,23 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
     g.waves = (uint32_t)S.cus * (uint32_t)(lnl::kSpanThreads / 64) * LNL_SPAN_ROUNDS;
     g.out = a.out;
     g.tab = S.span_tab;
-    void* scratch = nullptr;
-    const size_t bytes = lnl::span_scratch_words(a.n, g.waves) * sizeof(uint32_t);
-    hipError_t e = hipMallocAsync(&scratch, bytes, st);
-    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
-    lnl::span_scratch_layout(g, (uint32_t*)scratch);
-    int rc = 0;
-    e = lnl::launch_span(g, S.cus, st);
-    if (e != hipSuccess) rc = hip_fail(e, "span kernel launch");
-    if (rc == 0) {
-        lnl::BatchArgs o = a;
-        o.perm = g.ovf;
-        o.perm_n = g.ctl + 1;
-        o.span_rec = g.rec;
-        o.span_ctl = g.ctl;
-        o.span_tab = S.span_tab;
-        o.span_thdr = g.thdr;
-        rc = launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st, LNL_SPAN_FIX_WGS);
-    }
-    e = hipFreeAsync(scratch, st);
-    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
-    return rc;
+    std::lock_guard<std::mutex> lk(g_span_mu);
+    uint32_t* scratch = nullptr;
+    uint32_t parity = 0;
+    if (int rc = span_scratch(st, lnl::span_scratch_words(a.n, g.waves), &scratch, &parity)) return rc;
+    lnl::span_scratch_layout(g, scratch, parity);
+    if (span_ctl) *span_ctl = g.ctl;
+    hipError_t e = lnl::launch_span(g, S.cus, st);
+    if (e != hipSuccess) return hip_fail(e, "span kernel launch");
+    lnl::BatchArgs o = a;
+    o.perm = g.ovf;
+    o.perm_n = g.ctl + 1;
+    o.span_rec = g.rec;
+    o.span_ctl = g.ctl;
+    o.span_ctl_next = g.ctl_next;
+    o.span_tab = S.span_tab;
+    o.span_thdr = g.thdr;
+    return launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st, LNL_SPAN_FIX_WGS);
 }
 
 int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
@@ -902,7 +936,6 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     a.total = d_total;
     uint32_t* blk = (uint32_t*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);
     a.blk = blk;
-    a.span_waves = (uint32_t)S->cus * (uint32_t)(lnl::kSpanThreads / 64);
     void* tmp = (void*)(((uintptr_t)(blk + (size_t)lnl::kWalkBlock * n) + 255) & ~(uintptr_t)255);
     lnl::BatchArgs b{};
     b.base = d_base;
@@ -910,7 +943,9 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     b.n = n;
     b.ok = d_status;
     b.filter = 1u;
-    int rc = launch_csr_span(*S, b, st, lnl::kSpanFilter, blk);
+    const uint32_t* span_ctl = nullptr;
+    int rc = launch_csr_span(*S, b, st, lnl::kSpanFilter, blk, &span_ctl);
+    a.span_ctl = span_ctl;  // [2] != 0: the span kernel walked the batch
     if (rc == 0 && (e = lnl::launch_dispatch_walked(a, tmp, scan_bytes, st)) != hipSuccess)
         rc = hip_fail(e, "dispatch launch");
     e = hipFreeAsync(scratch, st);

@@ -38,7 +38,8 @@ struct BatchArgs {
     // optional (CSR span path): the span kernel's per-segment head / tail
     // records, completed first (crc32c_span.h); span_ctl[2] = segments
     const uint4* span_rec;
-    const uint32_t* span_ctl;   // [2] segments, [3] lines per segment
+    const uint32_t* span_ctl;   // [2] segments (0: take the whole batch, no perm), [3] lines per segment
+    uint32_t* span_ctl_next;    // the next call's control block: its overflow count is zeroed here
     const uint8_t* span_thdr;   // verify modes: header byte of each segment's tail datagram
     const uint32_t* span_tab;  // kSpanTabWords words (lnl_build_span_tables)
 };
@@ -179,8 +180,9 @@ struct SpanArgs {
     uint32_t waves;          // resident waves of the kernel's grid (CUs x 8)
     uint32_t* out;
     const uint32_t* tab;     // kSpanTabWords words (lnl_build_span_tables)
-    uint32_t* ctl;           // 4 words: [1] overflow datagrams, [2] segments
-    uint32_t* first;         // span_max_segments(waves) + 1
+    uint32_t* ctl;           // this call's control block: [1] overflow datagrams (0 on entry),
+                             // [2] segments (0: the batch kernel takes the whole batch), [3] R
+    uint32_t* ctl_next;      // the other block: the next call's, zeroed by this call's batch kernel
     uint32_t* ovf;           // n: datagrams left to the batch kernel
     uint4* rec;              // span_max_segments(waves) head / tail records
     // verify modes (kSpanVerify, kSpanFilter): ok[i] instead of out[i]; thdr:
@@ -195,7 +197,7 @@ struct SpanArgs {
     uint32_t* wblk;
 };
 size_t span_scratch_words(uint32_t n, uint32_t waves);
-void span_scratch_layout(SpanArgs& a, uint32_t* scratch);
+void span_scratch_layout(SpanArgs& a, uint32_t* scratch, uint32_t parity);
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream);
 
 // Outbound layer over a device burst (lnl_append.hip): datagram i of the CSR
@@ -292,10 +294,10 @@ struct DispatchArgs {
     uint32_t* pkt_parent;   // cap: datagram index
     uint32_t cap;
     uint32_t* total;        // device: packets delivered (may exceed cap)
-    // fused path (dispatch_fix_kernel): the span kernel's walk blocks, and the
-    // resident waves its geometry was computed for (to tell whether it ran)
+    // fused path (dispatch_fix_kernel): the span kernel's walk blocks, and its
+    // control block ([2] != 0: the span kernel took the batch and walked it)
     const uint32_t* blk;
-    uint32_t span_waves;
+    const uint32_t* span_ctl;
 };
 constexpr uint32_t kDispatchRec = 8;  // packets per datagram kept from the counting walk
 constexpr uint32_t kWalkBlock = 8;             // fused path: words per datagram block [count, 7 records]

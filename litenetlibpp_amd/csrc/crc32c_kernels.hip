@@ -277,7 +277,13 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
     // lanes itself): CRC = ~step^(-8e)(step^(1024 m) tail ^ head), tables read
     // from global memory
     if (a.span_rec) {
+        // the next call's overflow count starts from 0 (crc32c_span.h kSpanCtlWords)
+        if (blockIdx.x == 0 && threadIdx.x == 0 && a.span_ctl_next) a.span_ctl_next[1] = 0u;
         const uint32_t ns = a.span_ctl[2], Sb = a.span_ctl[3] << 7;
+        if (ns == 0u) {  // the span kernel did not take the batch: all of it here
+            a.perm = nullptr;
+            a.perm_n = nullptr;
+        }
         for (uint32_t g = 64u * (1u + blockIdx.x * kBlockThreads + threadIdx.x); g < ns;
              g += 64u * gridDim.x * kBlockThreads) {
             const uint4 h = a.span_rec[g];

@@ -20,6 +20,10 @@ namespace lnl {
 constexpr uint32_t kSpanRmin = 16;
 constexpr uint32_t kSpanRmax = 127;      // boundaries fit 16 bits (2 Sb < 65535); row powers m < 128
 constexpr uint32_t kSpanMaxRounds = 8;   // wave-batches per resident wave
+// Control block (words): [1] overflow count, [2] segments, [3] R.  A stream's
+// span scratch holds two, used by alternate calls: a call's batch kernel zeroes
+// the other block's count, so every call starts from 0 with no memset launch.
+constexpr uint32_t kSpanCtlWords = 8;
 
 struct SpanGeo {
     uint64_t S0;   // address of the stream's first line

@@ -61,9 +61,8 @@ constexpr uint32_t kEntry = 144;   // stash entry stride: 128 B of state + 16 B 
                                    // consecutive slots start on different banks and the 8
                                    // pieces of an entry sit at immediate offsets
 constexpr uint32_t kImageBytes = 8192;
-#ifndef LNL_SPAN_PREP_BLOCKS
-#define LNL_SPAN_PREP_BLOCKS 1024u  // pre-pass grid cap (256-thread workgroups, grid-stride; 1024 measured 1 % faster than 8192, 256 slower)
-#endif
+constexpr uint32_t kWin1 = 12;    // window chunks (64 offsets each) loaded ahead of the first rows
+
 #ifndef LNL_SPAN_PRIO
 #define LNL_SPAN_PRIO 0  // 0: progress-based issue priority; 1: static (experiment); 2: none
 #endif
@@ -81,6 +80,8 @@ constexpr uint32_t kMetaOff = kStashOff + kWaves * kStashBytes;
 constexpr uint32_t kProgOff = kMetaOff + kWaves * kCap * 8;  // rows done per wave (issue fairness)
 constexpr uint32_t kLdsBytes = kProgOff + kWaves * 4;
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
+constexpr uint32_t kWinMax = (kStashBytes / 4u) & ~63u;  // window entries the stash holds
+static_assert(kWinMax >= 64u * kWin1, "window");
 static_assert(kTabBytes % 16 == 0 && kStashOff % 16 == 0 && kMetaOff % 8 == 0, "LDS alignment");
 
 enum : uint32_t { kTypeNormal = 0, kTypeHead = 1, kTypeTail = 2 };
@@ -90,14 +91,8 @@ __device__ LNL_INLINE SpanGeo geometry_of(const SpanArgs& a) {
     return span_geometry(b + a.off[0], b + a.off[a.n], a.waves);
 }
 
-// ceil(P / (128 R)) for a byte offset P from S0 (lines < 2^32 whenever the
-// kernel runs: span_runs caps the batch at 64 W 8 segments of <= 127 lines)
-__device__ LNL_INLINE uint32_t seg_ceil(uint64_t P, uint32_t R) {
-    const uint32_t lines = (uint32_t)((P + 127u) >> 7);
-    return (lines + R - 1u) / R;
-}
 
-// ---- pre-pass ---------------------------------------------------------------
+// ---- helpers ------------------------------------------------------------------
 
 __device__ LNL_INLINE void append(uint32_t* cnt, uint32_t* list, bool take, uint32_t value) {
     const uint64_t m = __ballot(take);
@@ -111,39 +106,6 @@ __device__ LNL_INLINE void append(uint32_t* cnt, uint32_t* list, bool take, uint
 }
 
 __device__ LNL_INLINE uint32_t clamp16(int64_t v) { return v <= 0 ? 0u : (v >= 0xFFFF ? 0xFFFFu : (uint32_t)v); }
-
-// One thread per datagram: first[g] = min{ i : P_{i+1} > g Sb } for the g in
-// [ceil(P_i / Sb), ceil(P_{i+1} / Sb)) (first[NS] = n); CRC 0 for empty
-// datagrams; ctl[1] = 0 (the span kernel appends the overflow list), ctl[2] =
-// segments.  A batch the kernel does not take goes to the batch kernel whole.
-// (No atomics here, so the counters need no reset launch before it.)
-__global__ __launch_bounds__(256) void span_prep_kernel(SpanArgs a) {
-    const uint64_t b = (uint64_t)(uintptr_t)a.base - a.off0;
-    const SpanGeo G = geometry_of(a);
-    const bool whole = !span_runs(G, a.waves);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        a.ctl[1] = whole ? a.n : 0u;
-        a.ctl[2] = whole ? 0u : G.NS;
-        a.ctl[3] = G.R;
-    }
-    const uint32_t stride = gridDim.x * 256u;
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-        if (whole) {
-            a.ovf[i] = i;
-            continue;
-        }
-        const uint64_t Pi = b + a.off[i] - G.S0, Pj = b + a.off[i + 1] - G.S0;
-        if (Pi == Pj) {  // CRC-32C of zero bytes; a datagram too short for the layer
-            if (a.mode == kSpanCrc)
-                a.out[i] = 0u;
-            else
-                a.ok[i] = 0u;
-        }
-        const uint32_t lo = i == 0 ? 0u : seg_ceil(Pi, G.R), hi = seg_ceil(Pj, G.R);
-        for (uint32_t g = lo; g < hi; ++g) a.first[g] = i;
-        if (i + 1u == a.n) a.first[G.NS] = a.n;
-    }
-}
 
 // ---- the span kernel ---------------------------------------------------------
 
@@ -207,6 +169,13 @@ __device__ LNL_INLINE uint32_t phi_lds(const uint32_t* T, uint32_t tab_base, con
 // counted the other buffer's loads as older and drained both every step.
 __device__ LNL_INLINE void row_load(u32x4& v, uint64_t addr) {
     asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(addr) : "memory");
+}
+
+// 8 bytes (one offset) from global memory, in inline asm like row_load: the
+// setup's window loads are issued before the first rows' and waited for with a
+// counted vmcnt, so that the rows stay in flight meanwhile
+__device__ LNL_INLINE void off_load(uint64_t& v, uint64_t addr) {
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(addr) : "memory");
 }
 
 // 16 bytes to LDS at addr + OFF (immediate offset)
@@ -356,22 +325,17 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 #endif
     const uint64_t bsh = (uint64_t)(uintptr_t)A.base - A.off0;
     const SpanGeo G = geometry_of(A);
-    if (!span_runs(G, A.waves)) return;
+    const bool runs = span_runs(G, A.waves);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the batch kernel and the dispatch fix-up
+        A.ctl[2] = runs ? G.NS : 0u;             // 0: the whole batch is the batch kernel's
+        A.ctl[3] = G.R;
+    }
+    if (!runs) return;
     const uint32_t R = G.R, Sb = R << 7, NS = G.NS, nwb = G.nwb;
     if (blockIdx.x * kWaves >= nwb) return;  // whole workgroup idle (before the barrier)
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint32_t nw = gridDim.x * kWaves;
     const uint32_t n = A.n;
-    // the lane's first[] pair for wave-batch wb, fetched ahead (the first one
-    // before the tables go to LDS)
-    uint32_t su_k0, su_k1;
-    auto fetch = [&](uint32_t wb) {
-        const uint32_t g = wb * 64u + lane;
-        const bool ok = wb < nwb && g < NS;
-        su_k0 = ok ? A.first[g] : n;
-        su_k1 = ok ? A.first[g + 1u] : n;
-    };
-    fetch(gw);
     {
         const uint4* f = reinterpret_cast<const uint4*>(A.tab);
         uint4* fl = reinterpret_cast<uint4*>(lds + kTabOff);
@@ -380,6 +344,9 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         if (threadIdx.x < (uint32_t)kWaves) prog[threadIdx.x] = 0u;
         __syncthreads();
     }
+    // the wave's stash holds nothing until its first row: the setup's window
+    // of offsets goes there (int32, from the wave-batch's first byte)
+    int32_t* const win = reinterpret_cast<int32_t*>(lds + kStashOff + wave * kStashBytes);
     LNL_TL(1);
 #if LNL_SPAN_PRIO == 1
     if (wave >= 4u) __builtin_amdgcn_s_setprio(1);  // experiment: static priority for the younger waves
@@ -420,16 +387,106 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 }
             }
         };
-        u32x4 ra[8], rb[8];
-        issue(0u, ra);
-        issue(1u, rb);  // R >= 16
-
         // ---- this lane's datagrams ----------------------------------------
+        // [k0, k1): the datagrams ending in this segment; k0 = #{m >= 1 :
+        // pos(off[m]) <= segbase}.  Found without a pre-pass: (1) a = the same
+        // for the wave-batch's first byte, to within 64, from one interpolated
+        // probe of 64 offsets (a 64-ary search when the probe misses); (2) the
+        // window off[a ..] into LDS, loaded ahead of the first two rows and
+        // waited for with a counted vmcnt, so the rows stream meanwhile; (3)
+        // each lane's k0, its datagram's start and the next 16 ends from the
+        // window.  A window that does not reach the wave-batch's end (dense
+        // batches: > ~2,300 datagrams per wave-batch) leaves those lanes to
+        // global-memory searches.
         const uint32_t g = wb * 64u + lane;
         const bool live = g < NS;
         const uint64_t segbase = line0 + (uint64_t)lane * Sb;
-        const uint32_t k0 = su_k0;
-        const uint32_t k1 = su_k1;  // [k0, k1): datagrams ending in this segment
+        auto rel = [&](uint64_t o) -> int64_t { return (int64_t)(bsh + o - line0); };  // pos(o) - line0
+        uint32_t a;
+        {
+            const double f = (double)(line0 - G.S0) / (double)G.Pn;
+            const int64_t pi = (int64_t)(f * (double)n) - 32 * 64 + (int64_t)lane * 64;
+            const uint32_t idx = pi < 0 ? 0u : (pi > (int64_t)n ? n : (uint32_t)pi);
+            const uint64_t m = __ballot(rel(A.off[idx]) <= 0);
+            const uint32_t idx0 = (uint32_t)__shfl((int)idx, 0, 64), idx63 = (uint32_t)__shfl((int)idx, 63, 64);
+            if (m == 0ull && idx0 == 0u) {
+                a = 0u;
+            } else if (m != 0ull && !(m >> 63)) {  // the probe brackets it (m is a prefix of lanes)
+                a = (uint32_t)__shfl((int)idx, 63 - __builtin_clzll(m), 64);
+            } else {  // 64-ary search: rel(off[lo]) <= 0 (or lo = 0), rel(off[hi]) > 0
+                uint32_t lo = m == 0ull ? 0u : idx63, hi = m == 0ull ? idx0 : n;
+                while (hi - lo > 1u) {
+                    const uint32_t step = (hi - lo + 63u) >> 6;
+                    const uint32_t j = lo + lane * step;
+                    const uint64_t mm = __ballot(j < hi && rel(A.off[j]) <= 0);
+                    if (mm == 0ull) break;  // (lo = 0 and nothing <= line0)
+                    lo += (63u - (uint32_t)__builtin_clzll(mm)) * step;
+                    hi = lo + step < hi ? lo + step : hi;
+                }
+                a = lo;
+            }
+            a = uni(a);
+        }
+        auto win_value = [&](uint32_t m, uint64_t o) -> int32_t {  // window entry for off[m] = o
+            if (m > n) return 0x7FFFFFFF;
+            const int64_t r = rel(o);
+            return r > 0x7FFFFFFF ? 0x7FFFFFFF : (r < -0x7FFFFFFF ? -0x7FFFFFFF : (int32_t)r);
+        };
+        u32x4 ra[8], rb[8];
+        uint32_t wn;  // window entries
+        {
+            uint64_t wv[kWin1];
+#pragma unroll
+            for (int c = 0; c < (int)kWin1; ++c) {
+                const uint32_t mm = a + 64u * c + lane;
+                off_load(wv[c], (uint64_t)(uintptr_t)(A.off + (mm < n ? mm : n)));
+            }
+            issue(0u, ra);
+            issue(1u, rb);  // R >= 16
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the window; the rows stay in flight
+#pragma unroll
+            for (int c = 0; c < (int)kWin1; ++c) {
+                asm volatile("" : "+v"(wv[c]));
+                win[64u * c + lane] = win_value(a + 64u * c + lane, wv[c]);
+            }
+        }
+        wn = 64u * kWin1;
+        const int32_t tend = (int32_t)(64u * Sb);  // the wave-batch's end, from line0
+        // more of the window, while it does not reach past the wave-batch's
+        // end (these loads wait for the rows too)
+        while (wn < kWinMax && __shfl(win[wn - 1u], 0, 64) <= tend) {
+            const uint32_t mm = a + wn + lane;
+            win[wn + lane] = win_value(mm, A.off[mm < n ? mm : n]);
+            wn += 64u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int32_t wlast = win[wn - 1u];
+        uint32_t wtop = 1u;  // binary-search span: the smallest power of two >= wn
+        while (wtop < wn) wtop <<= 1;
+        // #{m >= 1 : pos(off[m]) <= line0 + t}: the window when it reaches past
+        // t, else a binary search of the offsets
+        auto count_le = [&](int32_t t) -> uint32_t {
+            if (wlast > t) {
+                uint32_t j = 0;
+                for (uint32_t step = wtop >> 1; step; step >>= 1)
+                    if (j + step < wn && win[j + step] <= t) j += step;
+                return a + j;
+            }
+            uint32_t lo = a, hi = n + 1u;
+            while (hi - lo > 1u) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (rel(A.off[mid]) <= (int64_t)t) lo = mid; else hi = mid;
+            }
+            return lo;
+        };
+        const int32_t tl0 = (int32_t)(lane * Sb);
+        const uint32_t k0 = live ? count_le(tl0) : n;
+        uint32_t k1 = (uint32_t)__shfl_down((int)k0, 1, 64);
+        if (lane == 63u) k1 = live ? count_le(tend) : n;
+        if (g == 0u)  // datagrams ending at the stream's first byte: all empty
+            for (uint32_t i = 0; i < k0; ++i) {
+                if (A.mode == kSpanCrc) A.out[i] = 0u; else A.ok[i] = 0u;
+            }
         Queue Q;
         uint32_t k = k0, kq, qn;
         int32_t cs;  // first byte of datagram k, from the segment's first byte
@@ -439,19 +496,28 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         uint32_t chdr = 0u;
         bool hdr_next = false;
         {
-            // the datagram's start and the next 16 boundaries, loaded together
-            // (indices clamped, values selected; the empty asm keeps the
-            // compiler from sinking each load into its own branch, which would
-            // wait for them one by one)
-            uint64_t ov[17];
+            // the datagram's start and the next 16 ends: from the window, or
+            // (past it) from global memory, loaded together (indices clamped,
+            // values selected; the empty asm keeps the compiler from sinking
+            // each load into its own branch, which would wait for them one by one)
+            int64_t ov[17];
+            if (k0 - a + 17u <= wn) {
 #pragma unroll
-            for (int j = 0; j < 17; ++j) {
-                const uint32_t kk = k0 + (uint32_t)j;
-                ov[j] = A.off[kk < n ? kk : n];
+                for (int j = 0; j < 17; ++j) ov[j] = (int64_t)win[k0 - a + (uint32_t)j] - (int64_t)tl0;
+            } else {
+                uint64_t ow[17];
+#pragma unroll
+                for (int j = 0; j < 17; ++j) {
+                    const uint32_t kk = k0 + (uint32_t)j;
+                    ow[j] = A.off[kk < n ? kk : n];
+                }
+#pragma unroll
+                for (int j = 0; j < 17; ++j) {
+                    asm volatile("" : "+v"(ow[j]));
+                    ov[j] = (int64_t)(bsh + ow[j]) - (int64_t)segbase;
+                }
             }
-#pragma unroll
-            for (int j = 0; j < 17; ++j) asm volatile("" : "+v"(ov[j]));
-            const int64_t d0 = k0 < n ? (int64_t)(bsh + ov[0]) - (int64_t)segbase : 0;
+            const int64_t d0 = k0 < n ? ov[0] : 0;
             cs = d0 < -(int64_t)(2u * Sb + 2u) ? -(int32_t)(2u * Sb + 2u) : (int32_t)d0;
             // the overflow list (datagrams touching three or more segments,
             // span_overflow): each has exactly one segment that no datagram
@@ -460,8 +526,8 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             uint32_t qp[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint32_t lo = clamp16((int64_t)(bsh + ov[2 * j + 1]) - (int64_t)segbase);
-                const uint32_t hi = clamp16((int64_t)(bsh + ov[2 * j + 2]) - (int64_t)segbase);
+                const uint32_t lo = clamp16(ov[2 * j + 1]);
+                const uint32_t hi = clamp16(ov[2 * j + 2]);
                 const uint32_t vlo = k0 + 2u * j < n ? lo : 0xFFFFu, vhi = k0 + 2u * j + 1u < n ? hi : 0xFFFFu;
                 qp[j] = vlo | (vhi << 16);
             }
@@ -848,8 +914,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             ev = is_open() && Q.front() <= rowend;
             while (__any(ev)) {
                 const uint32_t b = ev ? Q.front() - rowst : 128u;
-                const bool zero = ev && cs == (int32_t)(rowst + b);  // empty datagram (CRC written by the pre-pass)
+                const bool zero = ev && cs == (int32_t)(rowst + b);  // empty datagram: CRC 0, too short for the layer
                 const bool take = ev && !zero;                     // (started in this row: never a head)
+                if (zero) {
+                    if (A.mode == kSpanCrc) A.out[k] = 0u; else A.ok[k] = 0u;
+                }
                 if constexpr (WALK) walk_end(t, ev, b);
                 boundary(t, ev, zero, b, take, sout, nullptr);
                 if constexpr (WALK)
@@ -951,7 +1020,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                                   r_tail);
             if (A.mode != kSpanCrc) A.thdr[g] = (uint8_t)thdr;
         }
-        fetch(wb + nw);
     }
 #if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 16)
     LNL_TL(4);
@@ -966,28 +1034,27 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 
 }  // namespace
 
+// Scratch: two 8-word control blocks (crc32c_span.h kSpanCtl*), the overflow
+// list, the segment records and their tail header bytes.
 size_t span_scratch_words(uint32_t n, uint32_t waves) {
     const size_t ns = span_max_segments(waves);
-    size_t w = 4 + (ns + 1) + n;
+    size_t w = 2 * kSpanCtlWords + n;
     w = (w + 3) & ~(size_t)3;  // rec[] is 16-byte aligned
     return w + 4 * ns + (ns + 3) / 4;  // + thdr[ns]
 }
 
-void span_scratch_layout(SpanArgs& a, uint32_t* s) {
+void span_scratch_layout(SpanArgs& a, uint32_t* s, uint32_t parity) {
     const size_t ns = span_max_segments(a.waves);
-    a.ctl = s;
-    a.first = s + 4;
-    a.ovf = a.first + ns + 1;
-    size_t w = 4 + (ns + 1) + a.n;
+    a.ctl = s + kSpanCtlWords * (parity & 1u);
+    a.ctl_next = s + kSpanCtlWords * (~parity & 1u);
+    a.ovf = s + 2 * kSpanCtlWords;
+    size_t w = 2 * kSpanCtlWords + a.n;
     w = (w + 3) & ~(size_t)3;
     a.rec = reinterpret_cast<uint4*>(s + w);
     a.thdr = reinterpret_cast<uint8_t*>(a.rec + ns);
 }
 
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {
-    const uint32_t blocks = (a.n + 255u) / 256u;
-    const uint32_t prep = blocks < LNL_SPAN_PREP_BLOCKS ? blocks : LNL_SPAN_PREP_BLOCKS;
-    hipLaunchKernelGGL(span_prep_kernel, dim3(prep), dim3(256), 0, stream, a);
     if (a.wblk)
         hipLaunchKernelGGL(crc32c_span_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
     else

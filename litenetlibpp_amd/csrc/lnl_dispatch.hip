@@ -113,15 +113,14 @@ __global__ __launch_bounds__(256) void dispatch_count_kernel(DispatchArgs a) {
 // Keep the counts of accepted datagrams, zero the rest, move the records to
 // the slot-major layout the emit pass reads (coalesced here), and walk again
 // what a block cannot hold (8 or more packets) or what the span kernel did not
-// see (a batch it does not take, span_runs).
+// see (a batch it does not take: its control block says so).
 __global__ __launch_bounds__(256) void dispatch_fix_kernel(DispatchArgs a) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= a.n) return;
     const uint8_t st = a.status[i];
     uint32_t c = 0;
     if (st == 1u) {
-        const uint64_t b = (uint64_t)(uintptr_t)a.base - a.off0;
-        const bool walked = span_runs(span_geometry(b + a.off[0], b + a.off[a.n], a.span_waves), a.span_waves);
+        const bool walked = a.span_ctl[2] != 0u;  // (written by the span kernel of this call)
         const uint4* blk = reinterpret_cast<const uint4*>(a.blk + (size_t)i * kWalkBlock);
         const uint4 b0 = walked ? blk[0] : make_uint4(kWalkBlock, 0u, 0u, 0u);
         c = b0.x;
