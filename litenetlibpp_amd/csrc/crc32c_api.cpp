@@ -329,7 +329,8 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 #endif
 // The span path's scratch is kept per (device, stream) across calls: its two
 // control blocks (crc32c_span.h kSpanCtlWords) are used by alternate calls and
-// each call's batch kernel zeroes the other one's overflow count, so no call
+// each call's batch kernel zeroes the other one's overflow count, and its
+// wave-batch boundary flags are reset by the span kernel itself, so no call
 // needs a memset or a pre-pass launch.  It grows stream-ordered (hipFreeAsync /
 // hipMallocAsync on the stream), and the blocks are zeroed once when it does.
 // g_span_mu is held from the parity's choice through the launches, so a
@@ -342,7 +343,7 @@ struct SpanScratch {
 std::mutex g_span_mu;
 std::map<std::pair<int, hipStream_t>, SpanScratch> g_span_scratch;
 
-int span_scratch(hipStream_t st, size_t words, uint32_t** buf, uint32_t* parity) {
+int span_scratch(hipStream_t st, size_t words, size_t zero_words, uint32_t** buf, uint32_t* parity) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     SpanScratch& s = g_span_scratch[{dev, st}];
@@ -353,7 +354,7 @@ int span_scratch(hipStream_t st, size_t words, uint32_t** buf, uint32_t* parity)
         s.words = 0;
         hipError_t e = hipMallocAsync((void**)&s.buf, grow * sizeof(uint32_t), st);
         if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", grow * 4, hipGetErrorString(e));
-        e = hipMemsetAsync(s.buf, 0, 2 * lnl::kSpanCtlWords * sizeof(uint32_t), st);
+        e = hipMemsetAsync(s.buf, 0, zero_words * sizeof(uint32_t), st);
         if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
         s.words = grow;
         s.calls = 0;
@@ -386,7 +387,9 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
     std::lock_guard<std::mutex> lk(g_span_mu);
     uint32_t* scratch = nullptr;
     uint32_t parity = 0;
-    if (int rc = span_scratch(st, lnl::span_scratch_words(a.n, g.waves), &scratch, &parity)) return rc;
+    if (int rc = span_scratch(st, lnl::span_scratch_words(a.n, g.waves), lnl::span_scratch_zero_words(g.waves),
+                              &scratch, &parity))
+        return rc;
     lnl::span_scratch_layout(g, scratch, parity);
     if (span_ctl) *span_ctl = g.ctl;
     hipError_t e = lnl::launch_span(g, S.cus, st);
@@ -394,11 +397,8 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
     lnl::BatchArgs o = a;
     o.perm = g.ovf;
     o.perm_n = g.ctl + 1;
-    o.span_rec = g.rec;
     o.span_ctl = g.ctl;
     o.span_ctl_next = g.ctl_next;
-    o.span_tab = S.span_tab;
-    o.span_thdr = g.thdr;
     return launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st, LNL_SPAN_FIX_WGS);
 }
 

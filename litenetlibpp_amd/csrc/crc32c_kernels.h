@@ -35,13 +35,11 @@ struct BatchArgs {
     const uint32_t* perm_n;  // optional (device): number of perm entries, else n
     const uint32_t* tail_xor;  // optional: out[i] ^= tail_xor[i] for all i < n first (CSR uniform path)
     uint32_t xor_n;            // entries of tail_xor
-    // optional (CSR span path): the span kernel's per-segment head / tail
-    // records, completed first (crc32c_span.h); span_ctl[2] = segments
-    const uint4* span_rec;
-    const uint32_t* span_ctl;   // [2] segments (0: take the whole batch, no perm), [3] lines per segment
-    uint32_t* span_ctl_next;    // the next call's control block: its overflow count is zeroed here
-    const uint8_t* span_thdr;   // verify modes: header byte of each segment's tail datagram
-    const uint32_t* span_tab;  // kSpanTabWords words (lnl_build_span_tables)
+    // optional (CSR span path): the span kernel's control block ([2] == 0:
+    // it did not take the batch, so this kernel takes all of it) and the next
+    // call's, whose overflow count this kernel zeroes (crc32c_span.h)
+    const uint32_t* span_ctl;
+    uint32_t* span_ctl_next;
 };
 
 // Enqueue one batch kernel on `stream` with `grid` workgroups.
@@ -183,13 +181,11 @@ struct SpanArgs {
     uint32_t* ctl;           // this call's control block: [1] overflow datagrams (0 on entry),
                              // [2] segments (0: the batch kernel takes the whole batch), [3] R
     uint32_t* ctl_next;      // the other block: the next call's, zeroed by this call's batch kernel
+    uint32_t* xch;           // per wave-batch boundary: exchange block (crc32c_span.h kSpanXch*)
     uint32_t* ovf;           // n: datagrams left to the batch kernel
-    uint4* rec;              // span_max_segments(waves) head / tail records
-    // verify modes (kSpanVerify, kSpanFilter): ok[i] instead of out[i]; thdr:
-    // per segment, the header byte of its tail datagram
+    // verify modes (kSpanVerify, kSpanFilter): ok[i] instead of out[i]
     uint32_t mode;
     uint8_t* ok;
-    uint8_t* thdr;
     // filter + dispatch (kSpanFilter only; null otherwise): the MERGED walk of
     // every datagram, done by the lane its first byte streams through, into
     // one 8-word block per datagram: [count, record 0 .. 6] (kWalkPlain: not a
@@ -197,6 +193,7 @@ struct SpanArgs {
     uint32_t* wblk;
 };
 size_t span_scratch_words(uint32_t n, uint32_t waves);
+size_t span_scratch_zero_words(uint32_t waves);  // the leading words that must be 0 at allocation
 void span_scratch_layout(SpanArgs& a, uint32_t* scratch, uint32_t parity);
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream);
 

@@ -271,33 +271,14 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
             if (v) a.out[i] ^= v;
         }
     }
-    // CSR span path: complete the datagrams that entered a wave-batch's first
-    // segment from the previous wave-batch's last one (crc32c_span.hip leaves
-    // both parts as register values; it combines the heads of its other
-    // lanes itself): CRC = ~step^(-8e)(step^(1024 m) tail ^ head), tables read
-    // from global memory
-    if (a.span_rec) {
-        // the next call's overflow count starts from 0 (crc32c_span.h kSpanCtlWords)
+    // CSR span path (the span kernel combined the cross-segment heads itself):
+    // zero the next call's overflow count; take the whole batch when the span
+    // kernel did not
+    if (a.span_ctl) {
         if (blockIdx.x == 0 && threadIdx.x == 0 && a.span_ctl_next) a.span_ctl_next[1] = 0u;
-        const uint32_t ns = a.span_ctl[2], Sb = a.span_ctl[3] << 7;
-        if (ns == 0u) {  // the span kernel did not take the batch: all of it here
+        if (a.span_ctl[2] == 0u) {
             a.perm = nullptr;
             a.perm_n = nullptr;
-        }
-        for (uint32_t g = 64u * (1u + blockIdx.x * kBlockThreads + threadIdx.x); g < ns;
-             g += 64u * gridDim.x * kBlockThreads) {
-            const uint4 h = a.span_rec[g];
-            if (!(h.z & kSpanHeadBit) || h.y >= a.n) continue;
-            const uint32_t m = h.z & 0xFFu, e = (h.z >> 8) & 0xFFu;
-            const uint4 tr = a.span_rec[g - 1u];
-            const uint32_t crc = lnl_span_final(a.span_tab, e, lnl_span_rows(a.span_tab, m, tr.w) ^ h.x);
-            if constexpr (kMode == kModeVerify) {  // the whole datagram's CRC against the residue
-                const uint32_t len = (Sb - (tr.z >> kSpanTailShift)) + (m << 7) - e;
-                a.ok[h.y] = (uint8_t)lnl_span_status(a.filter ? kSpanFilter : kSpanVerify, crc, len,
-                                                     a.span_thdr[g - 1u]);
-            } else {
-                a.out[h.y] = crc;
-            }
         }
     }
     // entries to process: n, or a device-side count of perm entries

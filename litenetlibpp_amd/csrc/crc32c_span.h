@@ -64,21 +64,23 @@ LNL_HD LNL_INLINE bool span_overflow(uint64_t Pi, uint64_t Pj, uint32_t R) {
     return ge > gs + 1u;
 }
 
-// Per-segment record the kernel leaves for the fix-up: the head (the datagram
-// that entered from the previous segment and ends here) and the tail (the one
-// still open at the segment's end, ending in the next segment), as CRC
-// register values (lnl_span_phi below).
-//   x: the head's part in this segment   y: the head's datagram index
-//   z: m | e << 8 | head tracked << 16 | tail tracked << 17
-//      (m = rows from the segment start through the head's last row, e = bytes
-//      of that row after the head's last byte)
-//   w: the tail's part in this segment
-// Head CRC = ~step^(-8e)(step^(1024 m)(w of segment g-1) ^ x).
+// A head (the datagram that entered a segment from the previous one) and a
+// tail (the one still open at a segment's end) are folded to CRC register
+// values (lnl_span_phi below) and combined:
+//   head CRC = ~step^(-8e)(step^(1024 m)(tail) ^ head)
+// (m = rows from the segment start through the head's last row, e = bytes of
+// that row after the head's last byte).  Within a wave-batch the lanes combine
+// them through a shuffle; across wave-batches through an exchange block per
+// boundary in the stream's scratch (kSpanXch*).
+// hinfo word: m | e << 8 | head tracked << 16
 constexpr uint32_t kSpanHeadBit = 1u << 16;
-constexpr uint32_t kSpanTailBit = 1u << 17;
-// z >> kSpanTailShift: where the tail datagram starts, bytes from the segment's
-// first byte (< Sb <= 16,256: 14 bits)
-constexpr uint32_t kSpanTailShift = 18;
+// exchange block of wave-batch boundary w (words): the flag (arrivals: 0
+// between calls), the tail side (lane 63 of w - 1: its register value, its
+// datagram's start in the segment | header byte << 16) and the head side (lane
+// 0 of w: register value, datagram index, hinfo)
+constexpr uint32_t kSpanXchFlag = 0, kSpanXchTail = 1, kSpanXchTailInfo = 2, kSpanXchHead = 3,
+                   kSpanXchHeadIdx = 4, kSpanXchHeadInfo = 5;
+constexpr uint32_t kSpanXchWords = 8;  // one 32-byte sector per boundary
 
 // ---- verify modes ---------------------------------------------------------------
 // The span kernel checks a wire datagram (payload || LE32(CRC)) without

@@ -684,7 +684,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // ---- stash (wave-uniform counters) ---------------------------------
         uint32_t st_head = 0, st_tail = 0, head_slot = 0, tail_slot = 0;
         uint32_t hpos = 0, tpos = 0, r_head = 0, r_tail = 0, hk = 0, hinfo = 0, tcs = 0, thdr = 0;
-        bool hpend = false, tpend = false, htrack = false, ttrack = false;
+        bool hpend = false, tpend = false, htrack = false;
 
         // Fold the nf oldest entries, one per lane.  The caller's live state
         // (32 words) waits in the stash meanwhile -- lane l < nf in the slot
@@ -989,7 +989,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 if (!tdone) {
                     tpos = pos;
                     tpend = true;
-                    ttrack = true;
+
                     tcs = (uint32_t)cs;
                     thdr = chdr;
                 }
@@ -997,8 +997,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             }
         }
         // heads: CRC = ~step^(-8e)(step^(1024 m) tail ^ head), the tail from
-        // the previous lane; lane 0's from the previous wave-batch, so its
-        // record goes to the batch kernel's prologue
+        // the previous lane; lane 0's from the previous wave-batch (below)
         {
             const int src = (int)(lane - 1u) & 63;
             const uint32_t tprev = (uint32_t)__shfl((int)r_tail, src, 64);
@@ -1013,12 +1012,52 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     A.ok[hk] = (uint8_t)lnl_span_status(A.mode, crc, (Sb - tcs_prev) + (m << 7) - e, thdr_prev);
             }
         }
+        // Wave-batch boundaries: lane 0's head came in from wave-batch wb - 1's
+        // lane 63, lane 63's tail goes on to wb + 1's lane 0.  Each side writes
+        // its part into the boundary's exchange block (crc32c_span.h kSpanXch*)
+        // and then arrives at its flag; the side that arrives second has both
+        // parts and combines them, then resets the flag for the stream's next
+        // call.  The parts are device-scope (sc1) stores and loads and the flag
+        // a device-scope atomic, ordered by a vmcnt(0) between the stores and
+        // the arrival: no L2 writeback or invalidate (an acq_rel fence at agent
+        // scope does both on gfx950, per wave, and measured 35 us slower).
         if (live && (lane == 0u || lane == 63u)) {
-            A.rec[g] = make_uint4(r_head, hk,
-                                  hinfo | (htrack ? kSpanHeadBit : 0u) | (ttrack ? kSpanTailBit : 0u) |
-                                      (tcs << kSpanTailShift),
-                                  r_tail);
-            if (A.mode != kSpanCrc) A.thdr[g] = (uint8_t)thdr;
+            const uint32_t w = lane == 0u ? wb : wb + 1u;  // boundary w: segments 64 w - 1 | 64 w
+            if (w != 0u && w < nwb) {
+                uint32_t* const xb = A.xch + (size_t)w * kSpanXchWords;
+                auto put_x = [&](uint32_t i, uint32_t v) {
+                    __hip_atomic_store(xb + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
+                auto get_x = [&](uint32_t i) -> uint32_t {
+                    return __hip_atomic_load(xb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
+                if (lane == 0u) {
+                    put_x(kSpanXchHead, r_head);
+                    put_x(kSpanXchHeadIdx, hk);
+                    put_x(kSpanXchHeadInfo, hinfo | (htrack ? kSpanHeadBit : 0u));
+                } else {
+                    put_x(kSpanXchTail, r_tail);
+                    put_x(kSpanXchTailInfo, tcs | (thdr << 16));
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the parts are out before the arrival
+                if (__hip_atomic_fetch_add(xb + kSpanXchFlag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+                    const uint32_t head = lane == 0u ? r_head : get_x(kSpanXchHead);
+                    const uint32_t hidx = lane == 0u ? hk : get_x(kSpanXchHeadIdx);
+                    const uint32_t info = lane == 0u ? (hinfo | (htrack ? kSpanHeadBit : 0u)) : get_x(kSpanXchHeadInfo);
+                    const uint32_t tail = lane == 63u ? r_tail : get_x(kSpanXchTail);
+                    const uint32_t tinf = lane == 63u ? (tcs | (thdr << 16)) : get_x(kSpanXchTailInfo);
+                    if ((info & kSpanHeadBit) && hidx < n) {
+                        const uint32_t m = info & 0xFFu, e = (info >> 8) & 0xFFu;
+                        const uint32_t crc = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tail) ^ head);
+                        if (A.mode == kSpanCrc)
+                            A.out[hidx] = crc;
+                        else
+                            A.ok[hidx] = (uint8_t)lnl_span_status(A.mode, crc, (Sb - (tinf & 0xFFFFu)) + (m << 7) - e,
+                                                                  tinf >> 16);
+                    }
+                    __hip_atomic_store(xb + kSpanXchFlag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
         }
     }
 #if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 16)
@@ -1034,24 +1073,21 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 
 }  // namespace
 
-// Scratch: two 8-word control blocks (crc32c_span.h kSpanCtl*), the overflow
-// list, the segment records and their tail header bytes.
-size_t span_scratch_words(uint32_t n, uint32_t waves) {
-    const size_t ns = span_max_segments(waves);
-    size_t w = 2 * kSpanCtlWords + n;
-    w = (w + 3) & ~(size_t)3;  // rec[] is 16-byte aligned
-    return w + 4 * ns + (ns + 3) / 4;  // + thdr[ns]
+// Scratch: two 8-word control blocks (crc32c_span.h kSpanCtl*) and the
+// wave-batch boundaries' exchange blocks (kSpanXch*: their flags are zero
+// between calls, so all of it is zeroed once at allocation), then the overflow
+// list.
+size_t span_scratch_zero_words(uint32_t waves) {
+    return 2 * kSpanCtlWords + (size_t)(span_max_segments(waves) / 64u) * kSpanXchWords;
 }
 
+size_t span_scratch_words(uint32_t n, uint32_t waves) { return span_scratch_zero_words(waves) + n; }
+
 void span_scratch_layout(SpanArgs& a, uint32_t* s, uint32_t parity) {
-    const size_t ns = span_max_segments(a.waves);
     a.ctl = s + kSpanCtlWords * (parity & 1u);
     a.ctl_next = s + kSpanCtlWords * (~parity & 1u);
-    a.ovf = s + 2 * kSpanCtlWords;
-    size_t w = 2 * kSpanCtlWords + a.n;
-    w = (w + 3) & ~(size_t)3;
-    a.rec = reinterpret_cast<uint4*>(s + w);
-    a.thdr = reinterpret_cast<uint8_t*>(a.rec + ns);
+    a.xch = s + 2 * kSpanCtlWords;
+    a.ovf = s + span_scratch_zero_words(a.waves);
 }
 
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {

@@ -35,6 +35,8 @@ VARIANTS = {
     "prep8k": "-DLNL_SPAN_PREP_BLOCKS=8192u",       # span pre-pass: 8192 workgroups (before: 1 % slower than 1024)
     "prep256": "-DLNL_SPAN_PREP_BLOCKS=256u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
+    "fix8": "-DLNL_SPAN_FIX_WGS=8u",                # ... 8 workgroups
+    "fix1": "-DLNL_SPAN_FIX_WGS=1u",                # ... 1 workgroup
     "xcsr_dflt": "-DLNL_XOR_CSR_NT=0",              # flat CSR XOR: default cache policy
     "xcsr_u1": "-DLNL_XOR_CSR_U=1",                 # flat CSR XOR: 1 piece per lane and chunk (1 KiB)
     "xcsr_u4": "-DLNL_XOR_CSR_U=4",                 # flat CSR XOR: 4 pieces per lane and chunk (4 KiB)
