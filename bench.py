@@ -65,6 +65,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="untimed: run the step for this long before the warmup steps, so that the timed "
+                         "steps see the GPU's sustained clocks (compute-heavy steps run ~3 %% (config 2) to "
+                         "~15 %% (config 3) slower in the first milliseconds after idle; DESIGN 5); reported "
+                         "in the line as settle_ms / settle_steps")
     ap.add_argument("--workload", choices=["fixed", "csr", "filter", "xor", "xor_csr", "dispatch", "append",
                                            "filter_dispatch", "filter_then_dispatch"], default="fixed",
                     help="fixed: config 2 (the headline; config 4 at N = 8); csr: config 3; filter: the "
@@ -487,6 +492,17 @@ def main():
     if w.get("filter") and "status" not in w:
         w["status"] = torch.empty(w["n"], dtype=torch.uint8, device=device)
     stream = None if DRY else torch.cuda.current_stream()
+    # settle (untimed): the GPU ramps its clocks up under sustained load; the
+    # K timed steps below are exactly K steps of the workload either way
+    settle_steps = 0
+    if args.settle_ms > 0 and not DRY:
+        sync()
+        t_settle = time.perf_counter() + args.settle_ms * 1e-3
+        while time.perf_counter() < t_settle:
+            for _ in range(8):
+                launch(P, w, out, stream)
+            settle_steps += 8
+            sync()
     for _ in range(args.warmup):
         launch(P, w, out, stream)
     sync()
@@ -578,6 +594,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_ms": args.settle_ms if not DRY else 0.0,
+            "settle_steps": settle_steps,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
             "scaling": "weak",

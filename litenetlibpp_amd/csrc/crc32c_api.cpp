@@ -1009,13 +1009,20 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
         hipError_t e = lnl::launch_xor_flat(a, f, (int)grid, flat_v, (hipStream_t)hip_stream);
         return e == hipSuccess ? 0 : hip_fail(e, "xor flat launch");
     }
-    // CSR batches: the flat CSR kernel (whole pieces per lane over the batch's
-    // byte range; the range has no gaps, so no byte outside a datagram is
-    // written except by the two edge pieces' byte stores)
+    // CSR batches: the streaming CSR kernel (whole pieces per lane over the
+    // batch's byte range -- it has no gaps, so no byte outside a datagram is
+    // written except by the two edge pieces' byte stores -- the next 64 starts
+    // in registers; 117 VGPRs: 4 waves per SIMD, 4 workgroups of 4 waves per
+    // CU).  Experiments build: LNL_XOR_CSR_FLAT=1 the flat CSR kernel (round 2),
+    // 0 the per-datagram kernel.
 #ifndef LNL_XOR_CSR_FLAT
-#define LNL_XOR_CSR_FLAT 1
+#define LNL_XOR_CSR_FLAT 2
 #endif
-    if (LNL_XOR_CSR_FLAT && d_off) {
+    if (LNL_XOR_CSR_FLAT == 2 && d_off) {
+        hipError_t e = lnl::launch_xor_csr_stream(a, S->cus * 4, (hipStream_t)hip_stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "xor csr stream launch");
+    }
+    if (LNL_XOR_CSR_FLAT == 1 && d_off) {
         hipError_t e = lnl::launch_xor_csr_flat(a, S->cus * 8, (hipStream_t)hip_stream);
         return e == hipSuccess ? 0 : hip_fail(e, "xor csr flat launch");
     }

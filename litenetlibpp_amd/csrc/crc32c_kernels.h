@@ -272,6 +272,9 @@ hipError_t launch_xor_flat(const XorArgs& a, const FlatArgs& f, int grid, int va
 // flat CSR XOR (lnl_xor.hip): consecutive lanes own whole 16-byte pieces of the
 // batch's byte range; `grid` workgroups of 256 threads, each wave a run of chunks
 hipError_t launch_xor_csr_flat(const XorArgs& a, int grid, hipStream_t stream);
+// streaming CSR XOR (lnl_xor.hip, the product's CSR path): each wave a run of
+// 4 KiB chunks, the next 64 datagram starts in registers
+hipError_t launch_xor_csr_stream(const XorArgs& a, int grid, hipStream_t stream);
 
 // Delivered packets of a filtered burst (lnl_dispatch.hip): accepted
 // datagrams, MERGED containers cut into their packets.

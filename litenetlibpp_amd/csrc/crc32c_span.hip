@@ -86,6 +86,18 @@ static_assert(kTabBytes % 16 == 0 && kStashOff % 16 == 0 && kMetaOff % 8 == 0, "
 
 enum : uint32_t { kTypeNormal = 0, kTypeHead = 1, kTypeTail = 2 };
 
+// A datagram's result: its CRC (kSpanCrc) or its LNL_INBOUND_* status from the
+// whole-datagram CRC.  (The timeline build, LNL_SPAN_DIAG & 16, stores none:
+// out[] carries its stamps.)
+__device__ LNL_INLINE void store_result(const SpanArgs& A, uint32_t i, uint32_t crc, uint32_t len, uint32_t hdr) {
+#if !(defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 16))
+    if (A.mode == kSpanCrc)
+        A.out[i] = crc;
+    else
+        A.ok[i] = (uint8_t)lnl_span_status(A.mode, crc, len, hdr);
+#endif
+}
+
 __device__ LNL_INLINE SpanGeo geometry_of(const SpanArgs& a) {
     const uint64_t b = (uint64_t)(uintptr_t)a.base - a.off0;
     return span_geometry(b + a.off[0], b + a.off[a.n], a.waves);
@@ -317,7 +329,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 #if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 16)
     // diagnostic build only: per-wave timeline (s_memrealtime, 100 MHz) into
     // out[8 w ..] instead of CRCs
-    uint32_t tl[5];
+    uint32_t tl[8];
     tl[0] = (uint32_t)wall_clock64();
 #define LNL_TL(i) tl[i] = (uint32_t)wall_clock64()
 #else
@@ -336,22 +348,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint32_t nw = gridDim.x * kWaves;
     const uint32_t n = A.n;
-    {
-        const uint4* f = reinterpret_cast<const uint4*>(A.tab);
-        uint4* fl = reinterpret_cast<uint4*>(lds + kTabOff);
-        for (uint32_t i = threadIdx.x; i < kTabBytes / 16u; i += kThreads) fl[i] = f[i];
-        if (threadIdx.x == 0) *reinterpret_cast<uint4*>(lds + kZeroOff) = make_uint4(0u, 0u, 0u, 0u);
-        if (threadIdx.x < (uint32_t)kWaves) prog[threadIdx.x] = 0u;
-        __syncthreads();
-    }
-    // the wave's stash holds nothing until its first row: the setup's window
-    // of offsets goes there (int32, from the wave-batch's first byte)
-    int32_t* const win = reinterpret_cast<int32_t*>(lds + kStashOff + wave * kStashBytes);
-    LNL_TL(1);
-#if LNL_SPAN_PRIO == 1
-    if (wave >= 4u) __builtin_amdgcn_s_setprio(1);  // experiment: static priority for the younger waves
-#endif
-
     // per-lane addressing: load i brings piece pc of the row of lane 8 i + sub;
     // it lands in the image at that lane's row, slot pc ^ swz(8 i + sub)
     // (= pc ^ (sub >> 1) for even i, ^ 4 more for odd i)
@@ -362,38 +358,104 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
     const uint32_t r0 = image + lane * 128u + 16u * swz(lane);  // piece p of this lane's row: r0 ^ 16 p
     const uint64_t last_line = (G.S0 + G.Pn - 1u) & ~(uint64_t)127;
 
-    for (uint32_t wb = gw; wb < nwb; wb += nw) {
-        const uint64_t line0 = G.S0 + (uint64_t)wb * 64u * Sb;
-        const bool clamp = line0 + 64ull * Sb - 128u > last_line;
-        // row t of the wave-batch: load i of this lane is piece pc of line
-        // line0 + (8 i + sub) Sb + 128 t (clamped to the stream's last line in
-        // the last wave-batches)
-        const uint32_t last_rel = (uint32_t)(last_line - line0 < 0xFFFFFFFFull ? last_line - line0 : 0xFFFFFFFFull);
-        auto issue = [&](uint32_t t, u32x4* v) {
-            if (!clamp) {
-                const uint64_t rbase = line0 + ((uint64_t)t << 7);
-                uint32_t vo = voff;
-                asm volatile("" : "+v"(vo));  // 8 per-load addresses per row, not hoisted into 16 registers
+    // the current wave-batch: its first line, and whether its last rows are
+    // clamped to the stream's last line (the last wave-batches)
+    uint64_t line0 = 0;
+    bool clamp = false;
+    uint32_t last_rel = 0;
+    auto set_wb = [&](uint32_t wb) {
+        line0 = G.S0 + (uint64_t)wb * 64u * Sb;
+        clamp = line0 + 64ull * Sb - 128u > last_line;
+        last_rel = (uint32_t)(last_line - line0 < 0xFFFFFFFFull ? last_line - line0 : 0xFFFFFFFFull);
+    };
+    // row t of the wave-batch: load i of this lane is piece pc of line
+    // line0 + (8 i + sub) Sb + 128 t (clamped to the stream's last line)
+    auto issue = [&](uint32_t t, u32x4* v) {
+        if (!clamp) {
+            const uint64_t rbase = line0 + ((uint64_t)t << 7);
+            uint32_t vo = voff;
+            asm volatile("" : "+v"(vo));  // 8 per-load addresses per row, not hoisted into 16 registers
 #pragma unroll
-                for (int i = 0; i < 8; ++i) row_load(v[i], rbase + (uint64_t)(i * 8u * Sb) + vo);
-            } else {
-                uint32_t lo = (sub * Sb) + (t << 7);
-                asm volatile("" : "+v"(lo));
+            for (int i = 0; i < 8; ++i) row_load(v[i], rbase + (uint64_t)(i * 8u * Sb) + vo);
+        } else {
+            uint32_t lo = (sub * Sb) + (t << 7);
+            asm volatile("" : "+v"(lo));
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    uint32_t rel = lo + (uint32_t)i * 8u * Sb;
-                    rel = rel > last_rel ? last_rel : rel;
-                    row_load(v[i], line0 + rel + 16u * pc);
-                }
+            for (int i = 0; i < 8; ++i) {
+                uint32_t rel = lo + (uint32_t)i * 8u * Sb;
+                rel = rel > last_rel ? last_rel : rel;
+                row_load(v[i], line0 + rel + 16u * pc);
             }
-        };
+        }
+    };
+    // The setup's probe: 64 offsets 64 apart around the datagram whose start the
+    // wave-batch's first byte falls on, interpolated from its byte position
+    uint32_t pidx = 0;
+    uint64_t pv = 0;
+    auto probe = [&]() {
+        const double f = (double)(line0 - G.S0) / (double)G.Pn;
+        const int64_t pi = (int64_t)(f * (double)n) - 32 * 64 + (int64_t)lane * 64;
+        pidx = pi < 0 ? 0u : (pi > (int64_t)n ? n : (uint32_t)pi);
+        off_load(pv, (uint64_t)(uintptr_t)(A.off + pidx));
+    };
+    u32x4 ra[8], rb[8];
+    // The first wave-batch's probe and first two rows go out together with the
+    // fold tables' loads -- all inline asm, so the compiler waits for none of
+    // them -- and one counted vmcnt then waits for the probe and the tables
+    // only: the rows stream while the tables go to LDS and the probe is read.
+    {
+        const bool has0 = gw < nwb;
+        if (has0) {
+            set_wb(gw);
+            probe();
+        }
+        constexpr uint32_t kTabPieces = kTabBytes / 16u;
+        constexpr uint32_t kTabLoads = (kTabPieces + kThreads - 1u) / kThreads;
+        u32x4 tv[kTabLoads];
+#pragma unroll
+        for (uint32_t j = 0; j < kTabLoads; ++j) {
+            const uint32_t i = threadIdx.x + j * kThreads;
+            row_load(tv[j], (uint64_t)(uintptr_t)A.tab + 16u * (i < kTabPieces ? i : 0u));
+        }
+        if (has0) {
+            issue(0u, ra);
+            issue(1u, rb);  // R >= 16
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kTabLoads; ++j) {
+            const uint32_t i = threadIdx.x + j * kThreads;
+            if (i < kTabPieces) lds_write_piece(lds0 + kTabOff + 16u * i, tv[j]);
+        }
+        if (threadIdx.x == 0) lds_write_piece(lds0 + kZeroOff, (u32x4){0u, 0u, 0u, 0u});
+        if (threadIdx.x < (uint32_t)kWaves) prog[threadIdx.x] = 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // the wave's stash holds nothing until its first row: the setup's window
+    // of offsets goes there (int32, from the wave-batch's first byte)
+    int32_t* const win = reinterpret_cast<int32_t*>(lds + kStashOff + wave * kStashBytes);
+    LNL_TL(1);
+#if LNL_SPAN_PRIO == 1
+    if (wave >= 4u) __builtin_amdgcn_s_setprio(1);  // experiment: static priority for the younger waves
+#endif
+
+    for (uint32_t wb = gw; wb < nwb; wb += nw) {
+        if (wb != gw) {  // a later wave-batch (batches larger than one round): the same start
+            set_wb(wb);
+            probe();
+            issue(0u, ra);
+            issue(1u, rb);
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        }
         // ---- this lane's datagrams ----------------------------------------
         // [k0, k1): the datagrams ending in this segment; k0 = #{m >= 1 :
         // pos(off[m]) <= segbase}.  Found without a pre-pass: (1) a = the same
         // for the wave-batch's first byte, to within 64, from one interpolated
-        // probe of 64 offsets (a 64-ary search when the probe misses); (2) the
-        // window off[a ..] into LDS, loaded ahead of the first two rows and
-        // waited for with a counted vmcnt, so the rows stream meanwhile; (3)
+        // probe of 64 offsets, loaded with the first two rows (a 64-ary search
+        // when the probe misses); (2) the window off[a ..] into LDS; (3)
         // each lane's k0, its datagram's start and the next 16 ends from the
         // window.  A window that does not reach the wave-batch's end (dense
         // batches: > ~2,300 datagrams per wave-batch) leaves those lanes to
@@ -404,10 +466,9 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         auto rel = [&](uint64_t o) -> int64_t { return (int64_t)(bsh + o - line0); };  // pos(o) - line0
         uint32_t a;
         {
-            const double f = (double)(line0 - G.S0) / (double)G.Pn;
-            const int64_t pi = (int64_t)(f * (double)n) - 32 * 64 + (int64_t)lane * 64;
-            const uint32_t idx = pi < 0 ? 0u : (pi > (int64_t)n ? n : (uint32_t)pi);
-            const uint64_t m = __ballot(rel(A.off[idx]) <= 0);
+            asm volatile("" : "+v"(pv));  // (arrived: the counted wait above)
+            const uint32_t idx = pidx;
+            const uint64_t m = __ballot(rel(pv) <= 0);
             const uint32_t idx0 = (uint32_t)__shfl((int)idx, 0, 64), idx63 = (uint32_t)__shfl((int)idx, 63, 64);
             if (m == 0ull && idx0 == 0u) {
                 a = 0u;
@@ -432,7 +493,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             const int64_t r = rel(o);
             return r > 0x7FFFFFFF ? 0x7FFFFFFF : (r < -0x7FFFFFFF ? -0x7FFFFFFF : (int32_t)r);
         };
-        u32x4 ra[8], rb[8];
         uint32_t wn;  // window entries
         {
             uint64_t wv[kWin1];
@@ -441,9 +501,8 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint32_t mm = a + 64u * c + lane;
                 off_load(wv[c], (uint64_t)(uintptr_t)(A.off + (mm < n ? mm : n)));
             }
-            issue(0u, ra);
-            issue(1u, rb);  // R >= 16
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the window; the rows stay in flight
+            // the window (behind the first rows, which land first)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
             for (int c = 0; c < (int)kWin1; ++c) {
                 asm volatile("" : "+v"(wv[c]));
@@ -485,7 +544,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         if (lane == 63u) k1 = live ? count_le(tend) : n;
         if (g == 0u)  // datagrams ending at the stream's first byte: all empty
             for (uint32_t i = 0; i < k0; ++i) {
-                if (A.mode == kSpanCrc) A.out[i] = 0u; else A.ok[i] = 0u;
+                store_result(A, i, 0u, 0u, 0u);  // CRC 0; too short for the layer
             }
         Queue Q;
         uint32_t k = k0, kq, qn;
@@ -708,10 +767,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             const uint32_t type = (mt.y >> 8) & 3u, e = mt.y & 127u;  // mt.y: e | type << 8 | hdr << 10 | len << 18
             const uint32_t crc = final_crc_lds(tab_base, e, r);
             if (act && type == kTypeNormal && mt.x < n) {  // (the index check only guards the store)
-                if (A.mode == kSpanCrc)
-                    A.out[mt.x] = crc;
-                else
-                    A.ok[mt.x] = (uint8_t)lnl_span_status(A.mode, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
+                store_result(A, mt.x, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
             }
             // head / tail folds back to the lanes that own them
             const uint32_t hs = hpos - st_head, ts = tpos - st_head;
@@ -917,7 +973,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const bool zero = ev && cs == (int32_t)(rowst + b);  // empty datagram: CRC 0, too short for the layer
                 const bool take = ev && !zero;                     // (started in this row: never a head)
                 if (zero) {
-                    if (A.mode == kSpanCrc) A.out[k] = 0u; else A.ok[k] = 0u;
+                    store_result(A, k, 0u, 0u, 0u);
                 }
                 if constexpr (WALK) walk_end(t, ev, b);
                 boundary(t, ev, zero, b, take, sout, nullptr);
@@ -971,11 +1027,13 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 wlb = 0u;
             }
         }
-        // ---- the tail: the datagram still open, if it started here and ends
-        // in the next segment; then fold everything still waiting -----------
-        refill();
+        // ---- the tail: the datagram still open, if it started here; then
+        // fold everything still waiting.  (One that ends beyond the next
+        // segment is an overflow datagram: its tail is folded but not used --
+        // the next segment has no head -- and the batch kernel writes its CRC.
+        // So no boundary past the segment is needed here.) --------------------
         {
-            const bool tail = is_open() && k < n && cs >= 0 && cs < (int32_t)Sb && Q.front() <= 2u * Sb;
+            const bool tail = is_open() && k < n && cs >= 0 && cs < (int32_t)Sb;
             bool tdone = !tail;
             for (;;) {
                 const uint32_t nst = (uint32_t)__popcll(__ballot(!tdone));
@@ -996,6 +1054,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 tdone = true;
             }
         }
+        LNL_TL(4);
         // heads: CRC = ~step^(-8e)(step^(1024 m) tail ^ head), the tail from
         // the previous lane; lane 0's from the previous wave-batch (below)
         {
@@ -1006,12 +1065,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             if (htrack && lane != 0u && hk < n) {
                 const uint32_t m = hinfo & 0xFFu, e = (hinfo >> 8) & 0xFFu;
                 const uint32_t crc = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tprev) ^ r_head);
-                if (A.mode == kSpanCrc)
-                    A.out[hk] = crc;
-                else  // the head's length: its part in the previous segment and in this one
-                    A.ok[hk] = (uint8_t)lnl_span_status(A.mode, crc, (Sb - tcs_prev) + (m << 7) - e, thdr_prev);
+                // (the head's length: its part in the previous segment and in this one)
+                store_result(A, hk, crc, (Sb - tcs_prev) + (m << 7) - e, thdr_prev);
             }
         }
+        LNL_TL(5);
         // Wave-batch boundaries: lane 0's head came in from wave-batch wb - 1's
         // lane 63, lane 63's tail goes on to wb + 1's lane 0.  Each side writes
         // its part into the boundary's exchange block (crc32c_span.h kSpanXch*)
@@ -1049,11 +1107,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     if ((info & kSpanHeadBit) && hidx < n) {
                         const uint32_t m = info & 0xFFu, e = (info >> 8) & 0xFFu;
                         const uint32_t crc = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tail) ^ head);
-                        if (A.mode == kSpanCrc)
-                            A.out[hidx] = crc;
-                        else
-                            A.ok[hidx] = (uint8_t)lnl_span_status(A.mode, crc, (Sb - (tinf & 0xFFFFu)) + (m << 7) - e,
-                                                                  tinf >> 16);
+                        store_result(A, hidx, crc, (Sb - (tinf & 0xFFFFu)) + (m << 7) - e, tinf >> 16);
                     }
                     __hip_atomic_store(xb + kSpanXchFlag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
@@ -1061,11 +1115,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         }
     }
 #if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 16)
-    LNL_TL(4);
-    if (lane < 5u && 8u * gw + 8u <= n) {
+    LNL_TL(6);
+    if (lane < 7u && 8u * gw + 8u <= n) {
         uint32_t v = tl[0];
 #pragma unroll
-        for (int i = 1; i < 5; ++i) v = lane == (uint32_t)i ? tl[i] : v;
+        for (int i = 1; i < 7; ++i) v = lane == (uint32_t)i ? tl[i] : v;
         A.out[8u * gw + lane] = v;
     }
 #endif

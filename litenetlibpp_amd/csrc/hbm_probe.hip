@@ -180,11 +180,92 @@ __global__ __launch_bounds__(256) void seg_read_staged(const uint8_t* __restrict
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// forms 8-10: the config-2 lane-run kernel's access shape (crc32c_run.hip):
+// lane l of wave-batch w streams the kRunRS = 8 x 1400 bytes of its run, one
+// 128-byte line per step, lanes kRunRS apart, 8 lanes' lines per
+// wave-instruction; D = kLds + kVgpr rows in flight per wave, kLds of them by
+// LDS-DMA (read back as the lane's row), kVgpr into registers (XORed as
+// loaded: the probe does not transpose them).  Nothing is computed.
+//   form 8: 2 LDS-DMA rows (the run kernel today)
+//   form 9: 2 LDS-DMA + 2 VGPR rows
+//   form 10: 0 LDS-DMA + 4 VGPR rows
+constexpr uint32_t kRunRS = 8u * 1400u;
+constexpr uint32_t kRunRows = (kRunRS + 127u) / 128u;
+
+template <int kLds, int kVgpr>
+__global__ __launch_bounds__(256) void run_read(const uint8_t* __restrict__ p, uint32_t nruns,
+                                                uint32_t* __restrict__ sink) {
+    constexpr int D = kLds + kVgpr;
+    __shared__ __attribute__((aligned(16))) uint4 lds[4 * (kLds > 0 ? kLds : 1) * 512];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t gw = blockIdx.x * 4u + wave, nw = gridDim.x * 4u;
+    uint4* const bufs = lds + wave * (kLds > 0 ? kLds : 1) * 512;
+    const uint32_t sub = lane >> 3, piece = lane & 7u;
+    uint32_t acc = 0;
+    for (uint32_t wb = gw; wb * 64u < nruns; wb += nw) {
+        const uint8_t* base = p + (size_t)wb * 64u * kRunRS;
+        const uint32_t last = nruns - 1u - wb * 64u;
+        u32x4 v[kVgpr > 0 ? kVgpr : 1][8];
+        auto issue = [&](uint32_t t, int slot) {
+            if (t >= kRunRows) return;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t q = 8u * i + sub;
+                const uint32_t qq = q < last ? q : last;
+                // (the run's last row is a half line: stay inside the run, and
+                // so inside the buffer for the last one)
+                const uint32_t o = t * 128u + 16u * piece;
+                const uint8_t* src = base + (size_t)qq * kRunRS + (o < kRunRS - 16u ? o : kRunRS - 16u);
+                if (slot < kLds)
+                    __builtin_amdgcn_global_load_lds((const void*)src, (void*)(bufs + slot * 512 + 64 * i), 16, 0, 2);
+                else
+                    v[slot - kLds][i] = __builtin_nontemporal_load((const u32x4*)src);
+            }
+        };
+#pragma unroll
+        for (int j = 0; j < D; ++j) issue(j, j);
+        for (uint32_t t = 0; t < kRunRows; t += D) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                if (t + j >= kRunRows) break;
+                if (t + j + D <= kRunRows) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 * (D - 1)) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (j < kLds) {
+                    const uint4* r = bufs + j * 512 + lane * 8;
+                    uint4 x[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) x[k] = r[k];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) acc ^= x[k].x ^ x[k].w;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) acc ^= v[j - kLds][k].x ^ v[j - kLds][k].w;
+                }
+                issue(t + j + D, j);
+            }
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 extern "C" int lnl_probe_stream_read(const void* d, size_t bytes, uint32_t* d_sink, void* stream, int form) {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int grid = cus * 2;
+    if (form >= 8 && form <= 10) {
+        const size_t nruns = bytes / kRunRS;
+        if (nruns == 0 || nruns > 0xFFFFFFFFull) return -22;
+        const uint32_t nr = (uint32_t)nruns;
+        if (form == 8)
+            hipLaunchKernelGGL((run_read<2, 0>), dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d, nr, d_sink);
+        else if (form == 9)
+            hipLaunchKernelGGL((run_read<2, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d, nr, d_sink);
+        else
+            hipLaunchKernelGGL((run_read<0, 4>), dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)d, nr, d_sink);
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
     if (form >= 2 && form <= 7) {
         const size_t nseg = bytes / (kSegR * 128u);
         if (nseg == 0 || nseg > 0xFFFFFFFFull) return -22;

@@ -428,7 +428,183 @@ __global__ __launch_bounds__(256) void xor_csr_flat_kernel(XorArgs a, uint64_t M
     }
 }
 
+// (x mod K) for any 64-bit x: the 32-bit multiply path when x < 2^32 (every
+// datagram shorter than 4 GiB), a 64-bit remainder otherwise
+__device__ inline uint32_t mod_k64(uint64_t x, uint32_t K, uint64_t M) {
+    return (x >> 32) == 0u ? mod_k(x, K, M) : (uint32_t)(x % K);
+}
+
+// ---- streaming CSR kernel (the product's CSR path) ------------------------
+// The flat CSR kernel above places every piece among the next 64 starts with
+// a 6-step LDS search and loads those 64 starts once per chunk, after the
+// chunk before it has counted its own: a dependent round trip per 2 KiB.
+// Here a wave streams a contiguous run of 4 KiB chunks (4 pieces per lane,
+// coalesced dwordx4, the next chunk's loads issued before this chunk's
+// stores), and keeps the next 64 datagram starts in registers (one per lane),
+// reloaded only when a chunk reaches the 64th.  A chunk's pieces take their key
+// phase from the datagram start at or before them: a wave-uniform loop over
+// the few starts that fall inside the chunk (~6 per 4 KiB at config 3) -- no
+// per-piece search.  A start inside a piece splits its key into segments, as
+// in the flat kernels.
+constexpr uint32_t kStreamU = 4;                        // pieces per lane and chunk
+constexpr uint32_t kStreamChunk = 64u * kStreamU * 16u;  // 4 KiB per wave and chunk
+
+__global__ __launch_bounds__(256) void xor_csr_stream_kernel(XorArgs a, uint64_t M) {
+    __shared__ uint32_t ks[4][kKeyWords];
+    stage_key(a, ks);
+    __syncthreads();
+    const uint32_t K = a.key_len;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t ab = (uint64_t)((uintptr_t)a.base & 15u);  // buffer misalignment
+    uint8_t* const abase = a.base - ab;                       // 16-byte aligned
+    const uint64_t B0 = a.off[0] - a.off0 + ab, B1 = a.off[a.n] - a.off0 + ab;  // the batch, from abase
+    if (B1 <= B0) return;
+    const uint64_t S = B0 & ~(uint64_t)15;
+    const uint64_t chunks = (B1 - S + kStreamChunk - 1u) / kStreamChunk;
+    const uint64_t waves = (uint64_t)gridDim.x * 4u, gw = (uint64_t)blockIdx.x * 4u + w;
+    const uint64_t per = (chunks + waves - 1u) / waves;
+    const uint64_t c_begin = gw * per, c_end = c_begin + per < chunks ? c_begin + per : chunks;
+    if (c_begin >= c_end) return;
+    auto pos = [&](uint32_t d) -> uint64_t { return a.off[d] - a.off0 + ab; };
+    uint64_t C0 = S + c_begin * kStreamChunk;
+    // the datagram holding the run's first batch byte, its start, and the
+    // window of the next 64 starts (lane j: datagram dw + 1 + j; ~0 past n)
+    uint32_t dw = wave_datagram_of(a, ab, C0 < B0 ? B0 : C0);
+    uint64_t st_cur = pos(dw);
+    auto load_window = [&](uint32_t d) -> uint64_t {
+        const uint32_t dj = d + 1u + lane;
+        return dj <= a.n ? pos(dj) : ~0ull;
+    };
+    uint64_t sv = load_window(dw);
+    u32x4 v[kStreamU], nv[kStreamU];
+    auto load_chunk = [&](uint64_t c0, u32x4* dst) {
+#pragma unroll
+        for (int u = 0; u < (int)kStreamU; ++u) {
+            const uint64_t q = c0 + 16u * (lane + 64u * u);
+            if (q >= B0 && q + 16u <= B1) dst[u] = csr_load(reinterpret_cast<const u32x4*>(abase + q));
+        }
+    };
+    load_chunk(C0, v);
+    for (uint64_t c = c_begin; c < c_end; ++c, C0 += kStreamChunk) {
+        const uint64_t Cend = C0 + kStreamChunk;
+        if (c + 1u < c_end) load_chunk(Cend, nv);
+        // the window must hold every start up to the chunk's last byte (and
+        // one past it): slide it to the first start after C0 when it does not
+        // (re-anchored by a search when all 64 are behind C0)
+        {
+            const uint64_t top = __shfl(sv, 63, 64);
+            if (top != ~0ull && top < Cend) {
+                const uint64_t done = __ballot(sv <= C0);  // starts already behind: a prefix of lanes
+                if (done == ~0ull) {
+                    dw = wave_datagram_of(a, ab, C0 < B0 ? B0 : C0);
+                    st_cur = pos(dw);
+                } else {
+                    const uint32_t k = (uint32_t)__popcll(done);
+                    if (k > 0u) st_cur = __shfl(sv, (int)k - 1, 64);
+                    dw += k;
+                }
+                sv = load_window(dw);
+            }
+        }
+        // more than 64 starts in one chunk (datagrams under 64 bytes on
+        // average): the pieces search the offsets themselves (below)
+        const bool dense = __shfl(sv, 63, 64) != ~0ull && __shfl(sv, 63, 64) < Cend;
+        uint64_t q[kStreamU], sq[kStreamU];  // piece address, start at or before it
+        u32x4 key[kStreamU];
+        uint32_t seg[kStreamU];  // first byte of the piece's open key segment (0: none started inside)
+        // (a piece before the batch's first byte -- only the run's first
+        // piece, an edge piece -- starts its segment at that byte)
+        auto begin_piece = [&](int u, uint64_t start) {
+            sq[u] = start;
+            seg[u] = start > q[u] ? (uint32_t)(start - q[u] < 16u ? start - q[u] : 16u) : 0u;
+        };
+#pragma unroll
+        for (int u = 0; u < (int)kStreamU; ++u) {
+            q[u] = C0 + 16u * (lane + 64u * u);
+            key[u] = u32x4{0u, 0u, 0u, 0u};
+            begin_piece(u, st_cur);
+        }
+        if (!dense) {
+            // the starts inside (C0, Cend + 15]: ascending, a run of lanes
+            uint64_t in = __ballot(sv > C0 && sv < Cend + 16u);
+            while (in) {
+                const int j = __builtin_ctzll(in);
+                in &= in - 1u;
+                const uint64_t s = __shfl(sv, j, 64);
+#pragma unroll
+                for (int u = 0; u < (int)kStreamU; ++u) {
+                    if (s <= q[u]) {
+                        sq[u] = s;
+                    } else if (s < q[u] + 16u) {  // a datagram starts inside the piece
+                        const uint32_t b = (uint32_t)(s - q[u]);
+                        const uint32_t ph = seg[u] == 0u ? mod_k64(q[u] - sq[u], K, M)
+                                                         : (K - mod_k(seg[u], K, M)) % K;
+                        key[u] |= key_at(ks, ph) & byte_range((int)seg[u], (int)b);
+                        seg[u] = b;
+                    }
+                }
+            }
+        } else {
+            // dense chunk: each piece finds its own datagram (binary search)
+#pragma unroll
+            for (int u = 0; u < (int)kStreamU; ++u) {
+                if (q[u] + 16u <= B0 || q[u] >= B1) continue;
+                const uint64_t first_byte = q[u] < B0 ? B0 : q[u];
+                uint32_t lo = 0, hi = a.n;
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pos(mid) <= first_byte) lo = mid; else hi = mid;
+                }
+                begin_piece(u, pos(lo));
+                for (uint32_t d = lo + 1u; d <= a.n; ++d) {
+                    const uint64_t s = pos(d);
+                    if (s >= q[u] + 16u) break;
+                    if (s <= q[u]) { sq[u] = s; continue; }
+                    const uint32_t b = (uint32_t)(s - q[u]);
+                    const uint32_t ph = seg[u] == 0u ? mod_k64(q[u] - sq[u], K, M) : (K - mod_k(seg[u], K, M)) % K;
+                    key[u] |= key_at(ks, ph) & byte_range((int)seg[u], (int)b);
+                    seg[u] = b;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < (int)kStreamU; ++u) {
+            const uint64_t qa = q[u];
+            if (qa >= B1 || qa + 16u <= B0) continue;  // piece outside the batch
+            const uint32_t ph = seg[u] == 0u ? mod_k64(qa - sq[u], K, M) : (K - mod_k(seg[u], K, M)) % K;
+            key[u] |= key_at(ks, ph) & byte_range((int)seg[u], 16);
+            if (qa >= B0 && qa + 16u <= B1) {
+                csr_store(v[u] ^ key[u], reinterpret_cast<u32x4*>(abase + qa));
+            } else {  // the batch's edge piece: its own bytes only
+                uint8_t* bp = abase + qa;
+                for (uint32_t j = 0; j < 16u; ++j) {
+                    const uint64_t at = qa + j;
+                    if (at >= B0 && at < B1) bp[j] ^= (uint8_t)(key[u][j >> 2] >> (8 * (j & 3)));
+                }
+            }
+        }
+        // the next chunk's current start: the last start <= Cend (after a
+        // dense chunk the window does not reach it: search again)
+        if (!dense) {
+            const uint64_t done = __ballot(sv <= Cend);
+            if (done) st_cur = __shfl(sv, 63 - __builtin_clzll(done), 64);
+        } else if (c + 1u < c_end) {
+            dw = wave_datagram_of(a, ab, Cend);
+            st_cur = pos(dw);
+            sv = load_window(dw);
+        }
+#pragma unroll
+        for (int u = 0; u < (int)kStreamU; ++u) v[u] = nv[u];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_xor_csr_stream(const XorArgs& a, int grid, hipStream_t stream) {
+    const uint64_t M = ((1ull << 32) + a.key_len - 1u) / a.key_len;
+    hipLaunchKernelGGL(xor_csr_stream_kernel, dim3(grid), dim3(kThreads), 0, stream, a, M);
+    return hipGetLastError();
+}
 
 hipError_t launch_xor_csr_flat(const XorArgs& a, int grid, hipStream_t stream) {
     const uint64_t M = ((1ull << 32) + a.key_len - 1u) / a.key_len;

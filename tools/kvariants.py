@@ -42,6 +42,7 @@ VARIANTS = {
     "xcsr_u4": "-DLNL_XOR_CSR_U=4",                 # flat CSR XOR: 4 pieces per lane and chunk (4 KiB)
     "xcsr_u8": "-DLNL_XOR_CSR_U=8",                 # ... 8 (8 KiB)
     "xcsr_old": "-DLNL_XOR_CSR_FLAT=0",
+    "xcsr_flat": "-DLNL_XOR_CSR_FLAT=1",            # flat CSR XOR (round 2's product path)
     "xcsr_prev": "",                                # A/B slot: built from another lnl_xor.hip copied in by hand             # CSR XOR: the per-datagram kernel (before)
     "span_r2": "-DLNL_SPAN_ROUNDS=2u",              # CSR span: segments for two wave-batches per wave (static)
     "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)

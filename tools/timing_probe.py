@@ -35,8 +35,16 @@ def main():
     h = s.cuda_stream
     lib = P.lib()
 
-    def crc():
-        lib.lnl_crc32c_batch_fixed_dev(data.data_ptr(), L, L, n, out.data_ptr(), h)
+    if len(sys.argv) > 1 and sys.argv[1] == "csr":  # config 3 instead: 64..1400 B, CSR
+        lens = torch.randint(64, 1401, (n,), dtype=torch.int64, device=dev, generator=g)
+        off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        off[1:] = torch.cumsum(lens, 0)
+
+        def crc():
+            lib.lnl_crc32c_batch_csr_dev(data.data_ptr(), off.data_ptr(), n, out.data_ptr(), h)
+    else:
+        def crc():
+            lib.lnl_crc32c_batch_fixed_dev(data.data_ptr(), L, L, n, out.data_ptr(), h)
 
     pl = ctypes.CDLL(os.path.join(ROOT, "litenetlibpp_amd", "libhbm_probe.so"))
     pl.lnl_probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
