@@ -364,6 +364,30 @@ int span_scratch(hipStream_t st, size_t words, size_t zero_words, uint32_t** buf
     return 0;
 }
 
+// The CSR XOR kernel's chunk map (lnl_xor.hip), kept per (device, stream) like
+// the span scratch: each call's map kernel rewrites the words its XOR kernel
+// reads, in stream order, so calls on one stream share it.
+std::mutex g_xor_mu;
+std::map<std::pair<int, hipStream_t>, SpanScratch> g_xor_scratch;
+
+int xor_map_scratch(hipStream_t st, size_t words, uint32_t** buf) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_xor_mu);
+    SpanScratch& s = g_xor_scratch[{dev, st}];
+    if (s.words < words) {
+        const size_t grow = words + words / 4;
+        if (s.buf) (void)hipFreeAsync(s.buf, st);
+        s.buf = nullptr;
+        s.words = 0;
+        hipError_t e = hipMallocAsync((void**)&s.buf, grow * sizeof(uint32_t), st);
+        if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", grow * 4, hipGetErrorString(e));
+        s.words = grow;
+    }
+    *buf = s.buf;
+    return 0;
+}
+
 // CSR batches (product path): the span kernel (crc32c_span.hip: every line read
 // once, one 512-thread workgroup per CU; no pre-pass), then the batch kernel,
 // which completes the cross-wave-batch heads and takes the datagrams the span
@@ -1009,17 +1033,29 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
         hipError_t e = lnl::launch_xor_flat(a, f, (int)grid, flat_v, (hipStream_t)hip_stream);
         return e == hipSuccess ? 0 : hip_fail(e, "xor flat launch");
     }
-    // CSR batches: the streaming CSR kernel (whole pieces per lane over the
-    // batch's byte range -- it has no gaps, so no byte outside a datagram is
-    // written except by the two edge pieces' byte stores -- the next 64 starts
-    // in registers; 117 VGPRs: 4 waves per SIMD, 4 workgroups of 4 waves per
-    // CU).  Experiments build: LNL_XOR_CSR_FLAT=1 the flat CSR kernel (round 2),
-    // 0 the per-datagram kernel.
+    // CSR batches: the grid-interleaved CSR kernel (whole pieces per lane over
+    // the batch's byte range -- it has no gaps, so no byte outside a datagram
+    // is written except by the two edge pieces' byte stores -- chunk c to wave
+    // c mod W after a chunk-map kernel).  Experiments build: LNL_XOR_CSR_FLAT=2
+    // the streaming run kernel, 1 the flat CSR kernel (round 2), 0 the
+    // per-datagram kernel.
 #ifndef LNL_XOR_CSR_FLAT
-#define LNL_XOR_CSR_FLAT 2
+#define LNL_XOR_CSR_FLAT 3
+#endif
+#ifndef LNL_XOR_GRID_WGS
+#define LNL_XOR_GRID_WGS 4  // workgroups per CU (112 VGPRs: 4 waves per SIMD)
+#endif
+    if (LNL_XOR_CSR_FLAT == 3 && d_off) {
+        uint32_t* map = nullptr;
+        if (int rc = xor_map_scratch((hipStream_t)hip_stream, (size_t)n + 1u, &map)) return rc;
+        hipError_t e = lnl::launch_xor_csr_grid(a, map, n + 1u, S->cus * LNL_XOR_GRID_WGS, (hipStream_t)hip_stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "xor csr grid launch");
+    }
+#ifndef LNL_XOR_STREAM_WGS
+#define LNL_XOR_STREAM_WGS 6  // workgroups per CU
 #endif
     if (LNL_XOR_CSR_FLAT == 2 && d_off) {
-        hipError_t e = lnl::launch_xor_csr_stream(a, S->cus * 4, (hipStream_t)hip_stream);
+        hipError_t e = lnl::launch_xor_csr_stream(a, S->cus * LNL_XOR_STREAM_WGS, (hipStream_t)hip_stream);
         return e == hipSuccess ? 0 : hip_fail(e, "xor csr stream launch");
     }
     if (LNL_XOR_CSR_FLAT == 1 && d_off) {

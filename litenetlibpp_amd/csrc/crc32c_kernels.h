@@ -275,6 +275,10 @@ hipError_t launch_xor_csr_flat(const XorArgs& a, int grid, hipStream_t stream);
 // streaming CSR XOR (lnl_xor.hip, the product's CSR path): each wave a run of
 // 4 KiB chunks, the next 64 datagram starts in registers
 hipError_t launch_xor_csr_stream(const XorArgs& a, int grid, hipStream_t stream);
+// grid-interleaved CSR XOR (lnl_xor.hip, the product's CSR path): chunk c to
+// wave c mod W; `first` = cap >= 1 words of device scratch for the chunk map
+// (cap = n + 1 suffices: the map coarsens itself to fit)
+hipError_t launch_xor_csr_grid(const XorArgs& a, uint32_t* first, uint32_t cap, int grid, hipStream_t stream);
 
 // Delivered packets of a filtered burst (lnl_dispatch.hip): accepted
 // datagrams, MERGED containers cut into their packets.

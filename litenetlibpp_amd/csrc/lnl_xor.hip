@@ -438,16 +438,22 @@ __device__ inline uint32_t mod_k64(uint64_t x, uint32_t K, uint64_t M) {
 // The flat CSR kernel above places every piece among the next 64 starts with
 // a 6-step LDS search and loads those 64 starts once per chunk, after the
 // chunk before it has counted its own: a dependent round trip per 2 KiB.
-// Here a wave streams a contiguous run of 4 KiB chunks (4 pieces per lane,
-// coalesced dwordx4, the next chunk's loads issued before this chunk's
-// stores), and keeps the next 64 datagram starts in registers (one per lane),
+// Here a wave streams a contiguous run of 2 KiB chunks (2 pieces per lane,
+// coalesced dwordx4, the loads of the two chunks after it issued before this
+// chunk's stores), and keeps the next 64 datagram starts in registers (one per lane),
 // reloaded only when a chunk reaches the 64th.  A chunk's pieces take their key
 // phase from the datagram start at or before them: a wave-uniform loop over
-// the few starts that fall inside the chunk (~6 per 4 KiB at config 3) -- no
+// the few starts that fall inside the chunk (~3 per 2 KiB at config 3) -- no
 // per-piece search.  A start inside a piece splits its key into segments, as
 // in the flat kernels.
-constexpr uint32_t kStreamU = 4;                        // pieces per lane and chunk
-constexpr uint32_t kStreamChunk = 64u * kStreamU * 16u;  // 4 KiB per wave and chunk
+#ifndef LNL_XOR_STREAM_U
+#define LNL_XOR_STREAM_U 2  // pieces per lane and chunk
+#endif
+#ifndef LNL_XOR_STREAM_AHEAD
+#define LNL_XOR_STREAM_AHEAD 2  // chunks loaded ahead of the one being processed (1 or 2)
+#endif
+constexpr uint32_t kStreamU = LNL_XOR_STREAM_U;
+constexpr uint32_t kStreamChunk = 64u * kStreamU * 16u;  // bytes per wave and chunk
 
 __global__ __launch_bounds__(256) void xor_csr_stream_kernel(XorArgs a, uint64_t M) {
     __shared__ uint32_t ks[4][kKeyWords];
@@ -476,7 +482,7 @@ __global__ __launch_bounds__(256) void xor_csr_stream_kernel(XorArgs a, uint64_t
         return dj <= a.n ? pos(dj) : ~0ull;
     };
     uint64_t sv = load_window(dw);
-    u32x4 v[kStreamU], nv[kStreamU];
+    u32x4 v[kStreamU], nv[kStreamU], nv2[kStreamU];
     auto load_chunk = [&](uint64_t c0, u32x4* dst) {
 #pragma unroll
         for (int u = 0; u < (int)kStreamU; ++u) {
@@ -485,9 +491,14 @@ __global__ __launch_bounds__(256) void xor_csr_stream_kernel(XorArgs a, uint64_t
         }
     };
     load_chunk(C0, v);
+    if (LNL_XOR_STREAM_AHEAD == 2 && c_begin + 1u < c_end) load_chunk(C0 + kStreamChunk, nv);
     for (uint64_t c = c_begin; c < c_end; ++c, C0 += kStreamChunk) {
         const uint64_t Cend = C0 + kStreamChunk;
-        if (c + 1u < c_end) load_chunk(Cend, nv);
+        if (LNL_XOR_STREAM_AHEAD == 2) {
+            if (c + 2u < c_end) load_chunk(Cend + kStreamChunk, nv2);
+        } else if (c + 1u < c_end) {
+            load_chunk(Cend, nv);
+        }
         // the window must hold every start up to the chunk's last byte (and
         // one past it): slide it to the first start after C0 when it does not
         // (re-anchored by a search when all 64 are behind C0)
@@ -594,11 +605,238 @@ __global__ __launch_bounds__(256) void xor_csr_stream_kernel(XorArgs a, uint64_t
             sv = load_window(dw);
         }
 #pragma unroll
-        for (int u = 0; u < (int)kStreamU; ++u) v[u] = nv[u];
+        for (int u = 0; u < (int)kStreamU; ++u) {
+            v[u] = nv[u];
+            if (LNL_XOR_STREAM_AHEAD == 2) nv[u] = nv2[u];
+        }
+    }
+}
+
+// ---- grid-interleaved CSR kernel (the product's CSR path) -----------------
+// The run kernels above give each wave its own contiguous run of the batch:
+// ~6000 read+write streams hundreds of KiB apart, which the DRAM serves with
+// page misses and read/write turnarounds (both measured at 4.1-4.2 TB/s on the
+// config-3 batch, against 5.86 for the grid-stride fixed-stride kernel over
+// the same bytes).  Here chunk c goes to wave c mod W, so at any moment the
+// whole grid works inside one window of W x 2 KiB, as the fixed kernel does.
+// A wave's chunks are then W chunks apart, with nothing to carry between them:
+// chunk c's datagram comes from a chunk map, first[c] = the datagram holding
+// the chunk's first batch byte, written by a small map kernel launched before
+// (one thread per datagram marks the chunks whose first byte it holds).  The
+// 64 starts from first[c] on are one coalesced load (lane j: start of
+// first[c] + j).  A wave loads the next chunk's data, the next window and the
+// map word two chunks ahead before it keys and stores this chunk.  Waves are
+// numbered XCD-major, so neighbouring chunks -- which share offsets lines --
+// run under one L2.
+#ifndef LNL_XOR_GRID_U
+#define LNL_XOR_GRID_U 4  // pieces per lane and chunk (4 KiB chunks)
+#endif
+constexpr uint32_t kGridU = LNL_XOR_GRID_U;
+constexpr uint32_t kGridChunk = 64u * kGridU * 16u;  // 2 KiB per wave and chunk
+
+// map granularity: 2 KiB chunks, coarsened 2^k-fold until the map fits `cap`
+// words (batches averaging over 2 KiB per datagram)
+__device__ inline uint32_t map_shift(uint64_t chunks, uint32_t cap) {
+    uint32_t k = 0;
+    while (((chunks + (1ull << k) - 1u) >> k) > cap) ++k;
+    return k;
+}
+
+__global__ __launch_bounds__(256) void xor_chunk_map_kernel(XorArgs a, uint32_t* first, uint32_t cap) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t ab = (uint64_t)((uintptr_t)a.base & 15u);
+    const uint64_t B0 = a.off[0] - a.off0 + ab, B1 = a.off[a.n] - a.off0 + ab;
+    if (B1 <= B0) return;
+    const uint64_t S = B0 & ~(uint64_t)15;
+    const uint64_t chunks = (B1 - S + kGridChunk - 1u) / kGridChunk;
+    const uint32_t k = map_shift(chunks, cap);
+    const uint64_t G = (uint64_t)kGridChunk << k, blocks = (chunks + (1ull << k) - 1u) >> k;
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    uint64_t c_lo = 0, c_hi = 0;
+    if (i < a.n) {
+        const uint64_t Pi = a.off[i] - a.off0 + ab, Pj = a.off[i + 1] - a.off0 + ab;
+        if (Pj > Pi) {  // map blocks whose first byte S + m G lies in [Pi, Pj)
+            c_lo = Pi <= B0 ? 0u : (Pi - S + G - 1u) / G;
+            c_hi = (Pj - S + G - 1u) / G;
+            c_hi = c_hi < blocks ? c_hi : blocks;
+        }
+    }
+    // a datagram over 16 blocks: the whole wave writes its marks
+    const bool big = c_hi > c_lo + 16u;
+    uint64_t bigs = __ballot(big);
+    while (bigs) {
+        const int j = __builtin_ctzll(bigs);
+        bigs &= bigs - 1u;
+        const uint64_t lo = __shfl(c_lo, j, 64), hi = __shfl(c_hi, j, 64);
+        const uint32_t d = (uint32_t)__shfl((int)i, j, 64);
+        for (uint64_t c = lo + lane; c < hi; c += 64u) first[c] = d;
+    }
+    if (!big)
+        for (uint64_t c = c_lo; c < c_hi; ++c) first[c] = i;
+}
+
+__global__ __launch_bounds__(256) void xor_csr_grid_kernel(XorArgs a, uint64_t M, const uint32_t* first, uint32_t cap) {
+    __shared__ uint32_t ks[4][kKeyWords];
+    __shared__ u32x4 below[17];    // below[b]: bytes [0, b) of a piece
+    __shared__ uint32_t neg[16];   // neg[b] = -b mod K: the phase that puts key[0] on byte b
+    stage_key(a, ks);
+    const uint32_t K = a.key_len;
+    if (threadIdx.x < 17u) {
+        const int bb = (int)threadIdx.x;
+        u32x4 m;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int h = min(max(bb - 4 * w, 0), 4);
+            m[w] = (uint32_t)((1ull << (8 * h)) - 1u);
+        }
+        below[bb] = m;
+        if (bb < 16) neg[bb] = (K - (uint32_t)bb % K) % K;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t ab = (uint64_t)((uintptr_t)a.base & 15u);  // buffer misalignment
+    uint8_t* const abase = a.base - ab;                       // 16-byte aligned
+    const uint64_t B0 = a.off[0] - a.off0 + ab, B1 = a.off[a.n] - a.off0 + ab;  // the batch, from abase
+    if (B1 <= B0) return;
+    const uint64_t S = B0 & ~(uint64_t)15;
+    const uint64_t chunks = (B1 - S + kGridChunk - 1u) / kGridChunk;
+    const uint32_t mk = map_shift(chunks, cap);  // chunk c's map word: first[c >> mk]
+    // XCD-major wave numbering (workgroup b runs on XCD b mod 8)
+    const uint32_t G = gridDim.x;
+    const uint32_t vb = (G & 7u) == 0u ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint64_t W = (uint64_t)G * 4u, gw = (uint64_t)vb * 4u + w;
+    if (gw >= chunks) return;
+    auto pos = [&](uint32_t d) -> uint64_t { return a.off[d] - a.off0 + ab; };
+    auto load_chunk = [&](uint64_t c0, u32x4* dst) {
+#pragma unroll
+        for (int u = 0; u < (int)kGridU; ++u) {
+            const uint64_t q = c0 + 16u * (lane + 64u * u);
+            if (q >= B0 && q + 16u <= B1) dst[u] = csr_load(reinterpret_cast<const u32x4*>(abase + q));
+        }
+    };
+    // lane j: start of datagram d + j (~0 past the batch); lane 0 is d's own
+    auto window = [&](uint32_t d) -> uint64_t {
+        const uint32_t dj = d + lane;
+        return dj <= a.n ? pos(dj) : ~0ull;
+    };
+    // the key stream from byte b of a piece on, over bytes [b, 16)
+    auto restart = [&](u32x4 key, uint32_t b) -> u32x4 {
+        const u32x4 keep = below[b];
+        return (key & keep) | (key_at(ks, neg[b]) & ~keep);
+    };
+    uint64_t c = gw;
+    uint32_t d1 = c + W < chunks ? first[(c + W) >> mk] : 0u;
+    u32x4 v[kGridU], nv[kGridU];
+    load_chunk(S + c * kGridChunk, v);
+    uint64_t sv = window(first[c >> mk]);
+    for (; c < chunks; c += W) {
+        const uint64_t C0 = S + c * kGridChunk, Cend = C0 + kGridChunk;
+        const bool more = c + W < chunks;
+        uint64_t nsv = ~0ull;
+        uint32_t d2 = 0u;
+        if (more) {
+            load_chunk(C0 + W * kGridChunk, nv);
+            if (c + 2u * W < chunks) d2 = first[(c + 2u * W) >> mk];
+            nsv = window(d1);
+        }
+        // the window's datagram holds C0, or (coarse map) precedes it: the
+        // last of its starts <= C0 (none: the batch's first chunk, whose C0
+        // may precede the batch -- its first start counts as inside)
+        const uint64_t behind = __ballot(sv <= C0);
+        const int k0 = behind ? 63 - __builtin_clzll(behind) : 0;
+        const uint64_t st0 = __shfl(sv, k0, 64), top = __shfl(sv, 63, 64);
+        // the window ends inside the chunk (63 starts or more in it: datagrams
+        // under 32 bytes on average, or a coarse map far behind)
+        const bool dense = top != ~0ull && top < Cend;
+        u32x4 key[kGridU];
+        if (!dense) {
+            // chunk-relative starts inside (C0, Cend), ascending lanes; piece u
+            // of the lane covers chunk bytes [qr, qr + 16).  Pass 1: each
+            // piece's phase reference from the last start at or before it
+            // (phase = (qr + ref) mod K); pass 2: each start inside a piece
+            // restarts the key stream there.
+            const bool inside = sv > C0 && sv < Cend;
+            const uint32_t srel = inside ? (uint32_t)(sv - C0) : 0u;
+            const uint64_t ins = __ballot(inside);
+            const uint64_t lead = st0 <= C0 ? C0 - st0 : 0u;
+            const uint32_t base0 = mod_k64(lead, K, M);
+            uint32_t ref[kGridU];
+#pragma unroll
+            for (int u = 0; u < (int)kGridU; ++u) ref[u] = base0;
+            for (uint64_t in = ins; in; in &= in - 1u) {
+                const uint32_t sr = __builtin_amdgcn_readlane(srel, __builtin_ctzll(in));
+#pragma unroll
+                for (int u = 0; u < (int)kGridU; ++u)
+                    if (sr <= 16u * (lane + 64u * u)) ref[u] = 0u - sr;
+            }
+#pragma unroll
+            for (int u = 0; u < (int)kGridU; ++u) key[u] = key_at(ks, mod_k(16u * (lane + 64u * u) + ref[u], K, M));
+            for (uint64_t in = ins; in; in &= in - 1u) {
+                const uint32_t sr = __builtin_amdgcn_readlane(srel, __builtin_ctzll(in));
+#pragma unroll
+                for (int u = 0; u < (int)kGridU; ++u) {
+                    const uint32_t b = sr - 16u * (lane + 64u * u);  // start's byte in the piece
+                    if (b - 1u < 15u) key[u] = restart(key[u], b);
+                }
+            }
+        } else {
+            // dense chunk: each piece finds its own datagram (binary search)
+#pragma unroll
+            for (int u = 0; u < (int)kGridU; ++u) {
+                const uint64_t q = C0 + 16u * (lane + 64u * u);
+                key[u] = u32x4{0u, 0u, 0u, 0u};
+                if (q + 16u <= B0 || q >= B1) continue;
+                const uint64_t first_byte = q < B0 ? B0 : q;
+                uint32_t lo = 0, hi = a.n;
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pos(mid) <= first_byte) lo = mid; else hi = mid;
+                }
+                const uint64_t s0 = pos(lo);
+                key[u] = key_at(ks, s0 <= q ? mod_k64(q - s0, K, M) : 0u);
+                if (s0 > q) key[u] = restart(key[u], (uint32_t)(s0 - q));
+                for (uint32_t d = lo + 1u; d <= a.n; ++d) {
+                    const uint64_t s = pos(d);
+                    if (s >= q + 16u) break;
+                    if (s > q) key[u] = restart(key[u], (uint32_t)(s - q));
+                }
+            }
+        }
+        if (C0 >= B0 && Cend <= B1) {  // every piece whole inside the batch
+#pragma unroll
+            for (int u = 0; u < (int)kGridU; ++u)
+                csr_store(v[u] ^ key[u], reinterpret_cast<u32x4*>(abase + C0 + 16u * (lane + 64u * u)));
+        } else {
+#pragma unroll
+            for (int u = 0; u < (int)kGridU; ++u) {
+                const uint64_t qa = C0 + 16u * (lane + 64u * u);
+                if (qa >= B1 || qa + 16u <= B0) continue;  // piece outside the batch
+                if (qa >= B0 && qa + 16u <= B1) {
+                    csr_store(v[u] ^ key[u], reinterpret_cast<u32x4*>(abase + qa));
+                } else {  // the batch's edge piece: its own bytes only
+                    uint8_t* bp = abase + qa;
+                    for (uint32_t j = 0; j < 16u; ++j) {
+                        const uint64_t at = qa + j;
+                        if (at >= B0 && at < B1) bp[j] ^= (uint8_t)(key[u][j >> 2] >> (8 * (j & 3)));
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < (int)kGridU; ++u) v[u] = nv[u];
+        sv = nsv;
+        d1 = d2;
     }
 }
 
 }  // namespace
+
+hipError_t launch_xor_csr_grid(const XorArgs& a, uint32_t* first, uint32_t cap, int grid, hipStream_t stream) {
+    const uint64_t M = ((1ull << 32) + a.key_len - 1u) / a.key_len;
+    hipLaunchKernelGGL(xor_chunk_map_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, stream, a, first, cap);
+    hipLaunchKernelGGL(xor_csr_grid_kernel, dim3(grid), dim3(kThreads), 0, stream, a, M, (const uint32_t*)first, cap);
+    return hipGetLastError();
+}
 
 hipError_t launch_xor_csr_stream(const XorArgs& a, int grid, hipStream_t stream) {
     const uint64_t M = ((1ull << 32) + a.key_len - 1u) / a.key_len;

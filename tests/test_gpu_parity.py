@@ -919,6 +919,43 @@ def test_xor_layer_csr_runs_of_chunks(P):
     assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:5]}"
 
 
+@pytest.mark.parametrize("shape", ["mixed", "one", "clustered"])
+def test_xor_layer_csr_large_datagrams(P, shape):
+    """Batches averaging far over 2 KiB per datagram: the CSR kernel's chunk
+    map (one word per datagram + 1) coarsens to blocks of 2^k chunks, so a
+    chunk's map word names a datagram at or before it -- checked with mixed
+    sizes, one datagram of several MB, and runs of tiny datagrams between huge
+    ones (a window of 64 starts that ends before the chunk)."""
+    rng = np.random.default_rng({"mixed": 5, "one": 6, "clustered": 7}[shape])
+    key = rng.integers(0, 256, 29, dtype=np.uint8)
+    if shape == "mixed":
+        lens = rng.integers(0, 200000, 400)
+    elif shape == "one":
+        lens = np.array([5_000_003])
+    else:
+        parts = []
+        for _ in range(40):
+            parts.append(rng.integers(100000, 300000, 1))
+            parts.append(rng.integers(0, 40, int(rng.integers(1, 300))))
+        lens = np.concatenate(parts)
+    n = lens.size
+    lead = 11
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) + lead
+    total = int(off[-1]) + 9
+    g = torch.Generator(device="cuda")
+    g.manual_seed(23)
+    d = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=g)
+    src = d.cpu().numpy()
+    o = dev(off.view(np.int64), torch.int64)
+    P.xor_layer_csr(d, o, key.tobytes())
+    got = d.cpu().numpy()
+    phase = np.arange(int(off[-1]) - lead, dtype=np.int64) - np.repeat(off[:-1] - lead, lens)
+    exp = src.copy()
+    exp[lead:int(off[-1])] ^= key[phase % key.size]
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{n} datagrams: {bad.size} bytes differ, first at {bad[:5]}"
+
+
 @pytest.mark.parametrize("stride,length,klen,shift", [
     (1400, 1400, 10, 0), (1408, 1400, 10, 0), (64, 17, 10, 0), (1432, 1, 10, 0),
     (16, 16, 3, 0), (17, 17, 256, 0), (17, 5, 1, 0), (33, 32, 37, 0), (1400, 1400, 22, 0),

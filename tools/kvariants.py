@@ -43,6 +43,15 @@ VARIANTS = {
     "xcsr_u8": "-DLNL_XOR_CSR_U=8",                 # ... 8 (8 KiB)
     "xcsr_old": "-DLNL_XOR_CSR_FLAT=0",
     "xcsr_flat": "-DLNL_XOR_CSR_FLAT=1",            # flat CSR XOR (round 2's product path)
+    "xstr_u2a2w8": "-DLNL_XOR_CSR_FLAT=2 -DLNL_XOR_STREAM_U=2 -DLNL_XOR_STREAM_AHEAD=2 -DLNL_XOR_STREAM_WGS=8",
+    "xgrid_u2w5": "-DLNL_XOR_GRID_U=2 -DLNL_XOR_GRID_WGS=5",   # grid-interleaved CSR XOR: pieces per lane x workgroups per CU
+    "xgrid_u2w6": "-DLNL_XOR_GRID_U=2 -DLNL_XOR_GRID_WGS=6",
+    "xgrid_u3w5": "-DLNL_XOR_GRID_U=3 -DLNL_XOR_GRID_WGS=5",
+    "xgrid_u3w4": "-DLNL_XOR_GRID_U=3 -DLNL_XOR_GRID_WGS=4",
+    "xgrid_u4w3": "-DLNL_XOR_GRID_U=4 -DLNL_XOR_GRID_WGS=3",
+    "xgrid_u8w2": "-DLNL_XOR_GRID_U=8 -DLNL_XOR_GRID_WGS=2",
+    "xgrid_u1w8": "-DLNL_XOR_GRID_U=1 -DLNL_XOR_GRID_WGS=8",
+    "xgrid_dflt": "-DLNL_XOR_CSR_NT=0",             # ... default cache policy
     "xcsr_prev": "",                                # A/B slot: built from another lnl_xor.hip copied in by hand             # CSR XOR: the per-datagram kernel (before)
     "span_r2": "-DLNL_SPAN_ROUNDS=2u",              # CSR span: segments for two wave-batches per wave (static)
     "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)
@@ -243,6 +252,12 @@ def run(names, rounds, workloads):
             def call(L):
                 L.lnl_crc32c_batch_fixed_dev(data.data_ptr(), stride, L_pk, n_pk, out.data_ptr(), s.cuda_stream)
         times = {n: [] for n in names}
+        import time as _time
+        t_settle = _time.perf_counter() + 0.15  # sustained clocks first (bench.py --settle-ms)
+        while _time.perf_counter() < t_settle:
+            for n in names:
+                call(libs[n])
+            torch.cuda.synchronize()
         for r in range(rounds):
             for n in names:
                 e0 = torch.cuda.Event(enable_timing=True)
