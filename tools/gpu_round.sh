@@ -1,13 +1,29 @@
-# One GPU call (run via gpurun from the repo root): gpu tests, both benches,
-# CSR profile, kernel-variant timings.  Every step has its own time limit and
-# the script stops at the first failure.
+# Round GPU pass in two gpurun calls (each fits the 1200 s call limit):
+#   bash tools/gpu_round.sh <tag> tests      parity suite, smoke, every bench workload
+#   bash tools/gpu_round.sh <tag> profiles [workloads...]   rocprofv3 summaries
 set -o pipefail
-mkdir -p gpurun_out
-export TMPDIR=/tmp
-TAG=${1:-r01b}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAILED; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python -u bench.py > gpurun_out/bench_fixed.json 2> gpurun_out/bench_fixed.err && cat gpurun_out/bench_fixed.json || exit 1
-timeout -k 10 300 python -u bench.py --workload csr > gpurun_out/bench_csr.json 2> gpurun_out/bench_csr.err && cat gpurun_out/bench_csr.json || exit 1
-timeout -k 10 900 bash tools/profile_round.sh $TAG csr || exit 1
-timeout -k 10 300 python -u tools/kvariants.py run --names base,seg,seg_nofold,nocomp,nobucket --rounds 8 --workloads csr:1048576:64:1400 > gpurun_out/kv.log 2>&1 && cat gpurun_out/kv.log
+mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${1:?tag}
+MODE=${2:-tests}
+if [ "$MODE" = tests ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 || { echo PYTEST_FAILED; tail -30 gpurun_out/${TAG}_pytest.log; exit 1; }
+  tail -1 gpurun_out/${TAG}_pytest.log
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 && tail -1 gpurun_out/${TAG}_smoke.log || exit 1
+  timeout -k 10 300 python -u bench.py > gpurun_out/${TAG}_fixed.json 2> gpurun_out/${TAG}_fixed.err || exit 1
+  for w in csr filter xor xor_csr dispatch append filter_dispatch filter_then_dispatch; do
+    timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_$w.json 2> gpurun_out/${TAG}_$w.err || exit 1
+  done
+  for w in fixed csr filter xor xor_csr dispatch append filter_dispatch filter_then_dispatch; do
+    python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_$w.json'));r=d['roofline'];print('$w', d['ms_per_step'], r['frac'], r['kernel_ms'])" || exit 1
+  done
+  echo tests-done
+else
+  shift 2
+  WLS=${*:-fixed csr xor_csr append filter_dispatch}
+  for w in $WLS; do
+    timeout -k 10 400 bash tools/profile_round.sh $TAG $w || exit 1
+    PROFILES_DIR=gpurun_out/profiles_$TAG python3 tools/write_profiles.py $TAG $w > /dev/null || exit 1
+    rm -rf gpurun_out/prof_${TAG}_$w
+  done
+  echo profiles-done
+fi
