@@ -1057,25 +1057,43 @@ def test_full_config3_survey_recipe(P):
 
 
 # ---- outbound layer over a device burst (lnl_crc32c_append_csr_dev) ----------
-@pytest.mark.parametrize("case", ["mixed", "tiny_and_empty", "long"])
-def test_append_csr_matches_layer_outbound(P, case):
+APPEND_CASES = ["mixed", "tiny_and_empty", "long", "long_mix", "line_starts"]
+
+
+@pytest.mark.parametrize("align", ["dword", "odd"])
+@pytest.mark.parametrize("case", APPEND_CASES)
+def test_append_csr_matches_layer_outbound(P, case, align):
     """Every byte of the wire burst equals lnl_crc32c_layer_outbound (the CPU
     layer, called per datagram through the C ABI) of each payload, back to
     back; the CRCs equal the oracle's; nothing outside the burst is written
-    (guard bytes around an unaligned destination)."""
-    rng = np.random.default_rng(["mixed", "tiny_and_empty", "long"].index(case) + 900)
-    n = {"mixed": 20000, "tiny_and_empty": 30000, "long": 600}[case]
+    (guard bytes around the destination).  align: the destination a whole
+    number of dwords from the first payload byte, or not (every source / wire
+    phase the append kernel's shifted loads meet).  long_mix: overflow
+    datagrams (three or more span segments) inside a span batch; line_starts:
+    boundaries on 16-byte piece and 128-byte line starts, several per line,
+    runs of empty datagrams."""
+    rng = np.random.default_rng(APPEND_CASES.index(case) + 900 + (align == "odd") * 50)
+    n = {"mixed": 20000, "tiny_and_empty": 30000, "long": 600, "long_mix": 20000, "line_starts": 40000}[case]
     if case == "mixed":
         lens = rng.integers(0, 1501, n)
     elif case == "tiny_and_empty":
         lens = np.where(rng.random(n) < 0.3, 0, rng.integers(1, 40, n))
-    else:
+    elif case == "long":
         lens = rng.integers(2000, 40000, n)
+    elif case == "long_mix":
+        lens = np.where(rng.random(n) < 0.02, rng.integers(5000, 60000, n), rng.integers(0, 300, n))
+    else:
+        lens = rng.choice(np.array([0, 0, 1, 15, 16, 17, 112, 128, 128, 256, 384, 1024]), n)
     lead = int(rng.integers(0, 128))
     off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(lead)
     data = rng.integers(0, 256, int(off[-1]) + 5, dtype=np.uint8)
     size = int(off[-1] - off[0]) + 4 * n
+    # torch allocations are 256-byte aligned: (dst - first byte) % 4 = (shift - lead) % 4
     shift = int(rng.integers(1, 16))
+    if align == "dword":
+        shift = 16 + (lead % 4) if (shift - lead) % 4 else shift
+    elif (shift - lead) % 4 == 0:
+        shift += 1
     buf = torch.full((size + 64,), 0xA5, dtype=torch.uint8, device="cuda")
     wire, crc = P.append_csr(dev(data), dev(off.view(np.int64), torch.int64), out=buf[shift:shift + size],
                              want_crc=True)
@@ -1088,8 +1106,8 @@ def test_append_csr_matches_layer_outbound(P, case):
 
 
 def test_append_csr_config3_full(P):
-    """2^20 config-3 payloads (SURVEY recipe shape): CRCs bit-exact and the
-    first 50,000 datagrams' wire bytes exact; every CRC field holds its CRC."""
+    """2^20 config-3 payloads (SURVEY recipe shape): CRCs bit-exact, every CRC
+    field holds its CRC and every payload byte sits at its shift."""
     rng = np.random.default_rng(77)
     n = 1 << 20
     lens = rng.integers(64, 1401, n)
@@ -1102,10 +1120,13 @@ def test_append_csr_config3_full(P):
     exp_crc = oracle.batch_csr(data, off)
     assert np.array_equal(u32(crc), exp_crc)
     w = wire.cpu().numpy()
+    assert w.size == int(off[-1]) + 4 * n
     crcpos = off[1:].astype(np.int64) + 4 * np.arange(n)
     fields = w[crcpos[:, None] + np.arange(4)[None, :]].reshape(-1).view("<u4")
     assert np.array_equal(fields, exp_crc)
-    k = 50000
-    keep = np.ones(int(off[k]) + 4 * k, dtype=bool)
-    keep[(crcpos[:k, None] + np.arange(4)[None, :]).reshape(-1)] = False
-    assert np.array_equal(w[: keep.size][keep], data[: int(off[k])])
+    # every payload byte, in chunks of datagrams: byte x of datagram i at x + 4 i
+    for a in range(0, n, 1 << 16):
+        b = min(n, a + (1 << 16))
+        x = np.arange(int(off[a]), int(off[b]), dtype=np.int64)
+        x += 4 * np.repeat(np.arange(a, b, dtype=np.int64), lens[a:b])
+        assert np.array_equal(w[x], data[int(off[a]):int(off[b])]), f"payload bytes of datagrams {a}..{b}"
