@@ -29,6 +29,9 @@ constexpr int kThreads = 256;
 #define LNL_APPEND_TEAM 32  // measured: 16 lanes 559 us, 32 lanes 512 us, 64 lanes 613 us per config-3 call
 #endif
 constexpr uint32_t kTeam = LNL_APPEND_TEAM;  // lanes per datagram
+#ifndef LNL_APPEND_NT
+#define LNL_APPEND_NT 0  // nontemporal chunk stores (1), loads (2), both (3)
+#endif
 static_assert(kTeam >= 20 && kTeam <= 64, "one byte per lane covers the head (< 16) and tail (< 20) bytes");
 
 struct __attribute__((packed, aligned(4))) U4a {  // 16 bytes at a 4-byte aligned address
@@ -84,7 +87,12 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
 #pragma unroll 2
         for (uint64_t w = c0 + 16ull * q; w < c1; w += 16ull * kTeam) {
             const uint64_t sw = (w - delta) & ~(uint64_t)3;
+#if LNL_APPEND_NT & 2
+            const dev::u32x4 vv = __builtin_nontemporal_load(LNL_G(const dev::u32x4, sw));  // (4-byte aligned: unaligned dwordx4)
+            const U4a v = {vv[0], vv[1], vv[2], vv[3]};
+#else
             const U4a v = *LNL_G(const U4a, sw);
+#endif
             uint4 o = make_uint4(v.x, v.y, v.z, v.w);
             if (c) {  // (the fifth dword holds byte w - delta + 15, inside the payload)
                 const uint32_t v4 = *LNL_G(const uint32_t, sw + 16);
@@ -93,7 +101,11 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
                 o.z = __builtin_amdgcn_alignbyte(v.w, v.z, c);
                 o.w = __builtin_amdgcn_alignbyte(v4, v.w, c);
             }
+#if LNL_APPEND_NT & 1
+            __builtin_nontemporal_store(dev::u32x4{o.x, o.y, o.z, o.w}, LNL_G(dev::u32x4, w));
+#else
             *LNL_G(uint4, w) = o;
+#endif
         }
         if (b0) *LNL_G(uint8_t, x0) = v0;
         if (b1) *LNL_G(uint8_t, x1) = v1;

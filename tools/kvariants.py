@@ -32,6 +32,10 @@ VARIANTS = {
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
     "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
     "app_t64": "-DLNL_APPEND_TEAM=64",              # append kernel: 64 lanes per datagram (default 32)
+    "app_t16": "-DLNL_APPEND_TEAM=16",
+    "app_nts": "-DLNL_APPEND_NT=1",                 # append kernel: nontemporal chunk stores
+    "app_ntl": "-DLNL_APPEND_NT=2",                 # ... loads
+    "app_nt": "-DLNL_APPEND_NT=3",                  # ... both
     "prep8k": "-DLNL_SPAN_PREP_BLOCKS=8192u",       # span pre-pass: 8192 workgroups (before: 1 % slower than 1024)
     "prep256": "-DLNL_SPAN_PREP_BLOCKS=256u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
