@@ -176,11 +176,12 @@ def test_csr_bucketed_mix(P):
 
 
 @pytest.mark.parametrize("case", ["odd_n", "tiny", "line_multiples", "overflow_heavy"])
-def test_csr_pairs(P, case):
-    """CSR pair kernel (crc32c_pair.hip): a lone last datagram (odd n), pairs of
-    tiny datagrams sharing one line, lengths that end exactly on line
-    boundaries (unshared pairs), and many pairs too long for the pair buckets
-    (the batch-kernel overflow path)."""
+def test_csr_span_shared_lines(P, case):
+    """CSR batches through the product path (the span kernel and its overflow
+    batch kernel; shapes first written for round 1's pair kernel): an odd
+    count, runs of tiny datagrams sharing one line (several boundaries per lane
+    and row), lengths ending exactly on line boundaries, and one datagram in
+    eight long enough to cross three segments (the overflow list)."""
     rng = np.random.default_rng(["odd_n", "tiny", "line_multiples", "overflow_heavy"].index(case) + 300)
     n = {"odd_n": 30001, "tiny": 50000, "line_multiples": 20000, "overflow_heavy": 20000}[case]
     if case == "tiny":
@@ -202,11 +203,12 @@ def test_csr_pairs(P, case):
 
 
 @pytest.mark.parametrize("case", ["segment_multiples", "line_multiples", "lead_and_tail", "tiny_excess"])
-def test_csr_segments(P, case):
-    """Shapes aimed at the CSR segment kernel (crc32c_seg.hip): datagram ends on segment boundaries (lengths of 2 KiB multiples, the
-    segment size of batches this small), on line boundaries, a batch that
-    starts and ends mid-line, and segments with more ends than a lane tracks
-    (left to the batch kernel)."""
+def test_csr_span_segment_edges(P, case):
+    """CSR batches through the product path (the span kernel), at its segment
+    edges: datagram ends on segment boundaries (lengths of 2 KiB multiples,
+    the segment size of batches this small), on line boundaries, a batch that
+    starts and ends mid-line, and segments with more than 16 ends (queue
+    refills)."""
     rng = np.random.default_rng(["segment_multiples", "line_multiples", "lead_and_tail", "tiny_excess"].index(case) + 500)
     n = 40000
     if case == "segment_multiples":
@@ -226,7 +228,7 @@ def test_csr_segments(P, case):
     assert bad.size == 0, f"{case}: {bad.size} mismatches, first at {bad[:5]}"
 
 
-def test_csr_segments_several_batches_per_wave(P):
+def test_csr_span_several_wave_batches_per_wave(P):
     """A batch larger than one segment per lane at the largest segment size
     (> 2 GiB on 256 CUs): waves take several wave-batches."""
     rng = np.random.default_rng(600)
@@ -242,9 +244,10 @@ def test_csr_segments_several_batches_per_wave(P):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
 
 
-def test_csr_pairs_many_batches_per_wave(P):
-    """Far more pair batches than resident waves (persistent waves change
-    batch many times: descriptor slots, next-batch prefetch), small data."""
+def test_csr_span_dense_small_datagrams(P):
+    """1.2 M datagrams of 0-39 bytes (~24 MB): dense wave-batches whose offset
+    window does not reach their end (global-memory searches for those lanes),
+    many boundaries per row."""
     rng = np.random.default_rng(404)
     n = 1_200_000
     lens = rng.integers(0, 40, n)
