@@ -32,7 +32,7 @@ on this host over the WHOLE batch (copied to host memory, untimed), on one
 core and on every core this process may run on (rank 0, N = 1); the checker
 also compares the GPU's output for the whole batch with it.
 host_path: config 5 -- the same batch from pinned host memory through
-lnl_crc32c_batch_host (H2D + kernel + D2H on 2 streams), PCIe-inclusive.
+lnl_crc32c_batch_host (H2D + kernel + D2H on 4 streams), PCIe-inclusive.
 """
 from __future__ import annotations
 
@@ -402,7 +402,7 @@ def parity_sample(w, out, host):
 
 def host_path_rate(P, host, w, device):
     """Config 5: host-resident pinned batch -> lnl_crc32c_batch_host (H2D +
-    kernel + D2H over 2 streams).  PCIe-inclusive; never the headline value."""
+    kernel + D2H over 4 streams).  PCIe-inclusive; never the headline value."""
     data, off = host
     if off is None:
         off = np.arange(0, (w["n"] + 1) * w["L"], w["L"], dtype=np.uint64)
@@ -415,7 +415,7 @@ def host_path_rate(P, host, w, device):
     dt = (time.perf_counter() - t0) / reps
     return {"value": round(w["payload"] / dt / 1e9, 2), "unit": "GB/s",
             "what": "config 5: the same batch in pinned host memory through lnl_crc32c_batch_host "
-                    "(H2D + kernel + D2H, 2 streams, chunks of <= 64 Ki datagrams / 64 MiB), blocking, "
+                    "(H2D + kernel + D2H, 4 streams, chunks of <= 64 Ki datagrams / 64 MiB), blocking, "
                     f"mean of {reps} calls"}, got
 
 
@@ -437,7 +437,7 @@ def host_append_rate(P, host, w, device):
     ok = np.array_equal(wire[: int(woff[k])], w["wire"][: int(woff[k])].cpu().numpy())
     return {"value": round(w["payload"] / dt / 1e9, 2), "unit": "GB/s",
             "what": "the payload burst in pinned host memory through lnl_crc32c_append_host (H2D payload + "
-                    "offsets, CRC + append, D2H of the wire burst into pinned memory; 2 streams), blocking, "
+                    "offsets, CRC + append, D2H of the wire burst into pinned memory; 4 streams), blocking, "
                     "payload bytes / time, "
                     f"mean of {reps} calls",
             "parity": "wire bytes equal the device-resident call's" if ok else "MISMATCH"}

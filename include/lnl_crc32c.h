@@ -130,7 +130,7 @@ int lnl_inbound_filter_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uin
                                uint8_t* d_status, void* hip_stream);
 
 /* Host-resident batch (the socket path): copies h_base/h_off to `device`
- * in chunks over two HIP streams (H2D -> kernel -> D2H overlapped), writes
+ * in chunks over four HIP streams (H2D -> kernel -> D2H overlapped), writes
  * h_out[i], blocks until done.  h_off as in batch_csr_dev (h_off[0] may be
  * nonzero).  Pinned (hipHostMalloc / hipHostRegister) buffers give the full
  * PCIe rate; pageable ones work but copy through a staging buffer. */
@@ -196,7 +196,7 @@ int lnl_ingress_recv_batch(int fd, uint8_t* buf, size_t cap, uint64_t* off, uint
 /* Host-resident outbound layer (the send side of the socket path; SURVEY.md
  * 8(f) item 2): the payload burst, datagram i = h_payload[h_off[i] ..
  * h_off[i+1]) as in lnl_crc32c_batch_host (pinned
- * memory gives the full PCIe rate) goes H2D in chunks over two HIP streams,
+ * memory gives the full PCIe rate) goes H2D in chunks over four HIP streams,
  * through lnl_crc32c_append_csr_dev on `device`, and back D2H as the wire
  * burst: datagram i at h_wire + (h_off[i] - h_off[0]) + 4 i as
  * payload || LE32(CRC32C(payload)) -- the bytes lnl_crc32c_layer_outbound

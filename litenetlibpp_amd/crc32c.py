@@ -369,7 +369,7 @@ def _host_csr(data, offsets):
 
 def inbound_filter_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
     """Host-resident burst through the GPU inbound filter (H2D -> filter ->
-    D2H on 2 streams).  Blocking.  Returns uint8 status codes."""
+    D2H on 4 streams).  Blocking.  Returns uint8 status codes."""
     data, offsets = _host_csr(data, offsets)
     n = offsets.size - 1
     out = np.empty(max(n, 0), dtype=np.uint8)

@@ -53,6 +53,17 @@ int hip_fail(hipError_t e, const char* what) {
 
 constexpr int kMaxDevices = 64;
 
+// Host paths (lnl_crc32c_batch_host, lnl_inbound_filter_host,
+// lnl_crc32c_append_host): chunks go round-robin over this many streams, each
+// with its own staging buffers.  With two, a stream's next H2D waits behind its
+// own D2H, so the send side (a D2H as large as its H2D) overlapped the two
+// directions only half the time; from three on, the H2D of chunk k + 1 .. k + 3
+// runs while chunk k's wire burst comes back.
+#ifndef LNL_HOST_SLOTS
+#define LNL_HOST_SLOTS 4
+#endif
+constexpr int kHostSlots = LNL_HOST_SLOTS;
+
 struct DeviceState {
     std::once_flag once;
     int init_rc = 0;
@@ -65,11 +76,11 @@ struct DeviceState {
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)
     std::mutex host_mu;
-    hipStream_t streams[2] = {nullptr, nullptr};
-    uint8_t* d_bytes[2] = {nullptr, nullptr};
-    uint64_t* d_off[2] = {nullptr, nullptr};
-    uint32_t* d_out[2] = {nullptr, nullptr};
-    uint8_t* d_wire[2] = {nullptr, nullptr};  // append: the chunk's wire burst
+    hipStream_t streams[kHostSlots] = {};
+    uint8_t* d_bytes[kHostSlots] = {};
+    uint64_t* d_off[kHostSlots] = {};
+    uint32_t* d_out[kHostSlots] = {};
+    uint8_t* d_wire[kHostSlots] = {};  // append: the chunk's wire burst
     size_t cap_bytes = 0, cap_n = 0, cap_wire = 0;
 };
 
@@ -673,14 +684,15 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
 }
 }  // namespace
 
-// Host-resident batch: chunks of whole datagrams alternate over two streams;
-// each chunk is H2D (bytes + offsets) -> kernel (offsets rebased by off0) ->
-// D2H (CRCs).  Stream order makes buffer reuse safe; the two streams overlap
-// one chunk's copies with the other's kernel.
+// Host-resident batch: chunks of whole datagrams go round-robin over
+// kHostSlots streams; each chunk is H2D (bytes + offsets) -> kernel (offsets
+// rebased by off0) -> D2H (CRCs / statuses / the wire burst).  Stream order
+// makes buffer reuse safe; the streams overlap one chunk's copies with the
+// others' kernels and copies in the other direction.
 namespace {
 // Host-resident CSR batch through `device` (lnl_crc32c_batch_host,
-// lnl_inbound_filter_host, lnl_crc32c_append_host): chunks over two streams,
-// H2D -> kernel -> D2H.
+// lnl_inbound_filter_host, lnl_crc32c_append_host): chunks over kHostSlots
+// streams, H2D -> kernel -> D2H.
 enum HostMode : uint32_t { kHostCrc = 0, kHostFilter = 1, kHostAppend = 2 };
 // kHostCrc: h_out is u32 CRCs; kHostFilter: u8 inbound status codes;
 // kHostAppend: h_out is the wire burst (payload || LE32(CRC) per datagram,
@@ -721,12 +733,12 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         }
     }
     if (!S->streams[0]) {
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < kHostSlots; ++k)
             if ((e = hipStreamCreateWithFlags(&S->streams[k], hipStreamNonBlocking)) != hipSuccess)
                 return hip_fail(e, "hipStreamCreate");
     }
     if (need_bytes > S->cap_bytes || need_n > S->cap_n) {
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kHostSlots; ++k) {
             (void)hipFree(S->d_bytes[k]);
             (void)hipFree(S->d_off[k]);
             (void)hipFree(S->d_out[k]);
@@ -738,7 +750,7 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         }
         S->cap_bytes = S->cap_n = S->cap_wire = 0;
         const size_t nb = std::max<size_t>(need_bytes, 256);
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kHostSlots; ++k) {
             if ((e = hipMalloc(&S->d_bytes[k], nb)) != hipSuccess ||
                 (e = hipMalloc(&S->d_off[k], (size_t)(need_n + 1) * 8)) != hipSuccess ||
                 (e = hipMalloc(&S->d_out[k], (size_t)need_n * 4)) != hipSuccess)
@@ -749,12 +761,12 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
     }
     const size_t need_wire = S->cap_bytes + (size_t)S->cap_n * LNL_CRC32C_LAYER_EXTRA;
     if (mode == kHostAppend && need_wire > S->cap_wire) {  // the wire staging, on the first append only
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kHostSlots; ++k) {
             (void)hipFree(S->d_wire[k]);
             S->d_wire[k] = nullptr;
         }
         S->cap_wire = 0;
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < kHostSlots; ++k)
             if ((e = hipMalloc(&S->d_wire[k], need_wire)) != hipSuccess)
                 return fail(-ENOMEM, "wire staging allocation: %s", hipGetErrorString(e));
         S->cap_wire = need_wire;
@@ -762,7 +774,7 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
     // after the first enqueue, every error path drains both streams first: the
     // caller may free h_base / h_out as soon as we return
     auto drained = [&](int rc) {
-        for (int s2 = 0; s2 < 2; ++s2) (void)hipStreamSynchronize(S->streams[s2]);
+        for (int s2 = 0; s2 < kHostSlots; ++s2) (void)hipStreamSynchronize(S->streams[s2]);
         return rc;
     };
     uint32_t i = 0;
@@ -797,7 +809,7 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
                              hipSuccess)
                 return drained(hip_fail(e, "D2H crc"));
             i = j;
-            k ^= 1;
+            k = (k + 1) % kHostSlots;
             continue;
         }
         if (filter) {
@@ -812,9 +824,9 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
                                 hipMemcpyDeviceToHost, st)) != hipSuccess)
             return drained(hip_fail(e, "D2H"));
         i = j;
-        k ^= 1;
+        k = (k + 1) % kHostSlots;
     }
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < kHostSlots; ++s)
         if ((e = hipStreamSynchronize(S->streams[s])) != hipSuccess) return drained(hip_fail(e, "hipStreamSynchronize"));
     return 0;
 }

@@ -10,9 +10,12 @@ if [ "$MODE" = tests ]; then
   tail -1 gpurun_out/${TAG}_pytest.log
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 && tail -1 gpurun_out/${TAG}_smoke.log || exit 1
   timeout -k 10 300 python -u bench.py > gpurun_out/${TAG}_fixed.json 2> gpurun_out/${TAG}_fixed.err || exit 1
-  for w in csr filter xor xor_csr dispatch append filter_dispatch filter_then_dispatch; do
+  for w in csr filter xor xor_csr dispatch filter_dispatch filter_then_dispatch; do
     timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_$w.json 2> gpurun_out/${TAG}_$w.err || exit 1
   done
+  # the send side from pinned host memory too (host_append)
+  timeout -k 10 300 python -u bench.py --workload append --no-cpu-baseline > gpurun_out/${TAG}_append.json 2> gpurun_out/${TAG}_append.err || exit 1
+  python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_append.json'));print('host_append', d.get('host_append', {}).get('value'), 'GB/s')" || exit 1
   for w in fixed csr filter xor xor_csr dispatch append filter_dispatch filter_then_dispatch; do
     python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_$w.json'));r=d['roofline'];print('$w', d['ms_per_step'], r['frac'], r['kernel_ms'])" || exit 1
   done
