@@ -101,14 +101,20 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
                 o.z = __builtin_amdgcn_alignbyte(v.w, v.z, c);
                 o.w = __builtin_amdgcn_alignbyte(v4, v.w, c);
             }
-#if LNL_APPEND_NT & 1
+#if defined(LNL_APPEND_DIAG) && (LNL_APPEND_DIAG & 2)
+            if (w == 7u) *LNL_G(uint4, w) = o;  // diagnostic build only: no chunk stores (wrong burst)
+#elif LNL_APPEND_NT & 1
             __builtin_nontemporal_store(dev::u32x4{o.x, o.y, o.z, o.w}, LNL_G(dev::u32x4, w));
 #else
             *LNL_G(uint4, w) = o;
 #endif
         }
+#if defined(LNL_APPEND_DIAG) && (LNL_APPEND_DIAG & 1)
+        if (x0 == 7u && x1 == 9u) *LNL_G(uint8_t, x0) = v0 ^ v1;  // diagnostic build only: no head / tail stores (wrong burst)
+#else
         if (b0) *LNL_G(uint8_t, x0) = v0;
         if (b1) *LNL_G(uint8_t, x1) = v1;
+#endif
     }
 }
 

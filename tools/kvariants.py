@@ -36,6 +36,9 @@ VARIANTS = {
     "app_nts": "-DLNL_APPEND_NT=1",                 # append kernel: nontemporal chunk stores
     "app_ntl": "-DLNL_APPEND_NT=2",                 # ... loads
     "app_nt": "-DLNL_APPEND_NT=3",                  # ... both
+    "app_nohead": "-DLNL_APPEND_DIAG=1",            # append kernel: no head / tail byte stores (wrong burst)
+    "app_nochunk": "-DLNL_APPEND_DIAG=2",           # ... no chunk stores (wrong burst)
+    "app_nostore": "-DLNL_APPEND_DIAG=3",           # ... no stores at all (wrong burst)
     "prep8k": "-DLNL_SPAN_PREP_BLOCKS=8192u",       # span pre-pass: 8192 workgroups (before: 1 % slower than 1024)
     "prep256": "-DLNL_SPAN_PREP_BLOCKS=256u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
