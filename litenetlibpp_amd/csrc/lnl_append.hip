@@ -29,6 +29,9 @@ constexpr int kThreads = 256;
 #define LNL_APPEND_TEAM 32  // measured: 16 lanes 559 us, 32 lanes 512 us, 64 lanes 613 us per config-3 call
 #endif
 constexpr uint32_t kTeam = LNL_APPEND_TEAM;  // lanes per datagram
+#ifndef LNL_APPEND_WGS
+#define LNL_APPEND_WGS 16u  // workgroups per CU (teams stride over the datagrams)
+#endif
 #ifndef LNL_APPEND_NT
 #define LNL_APPEND_NT 0  // nontemporal chunk stores (1), loads (2), both (3)
 #endif
@@ -123,7 +126,7 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
 hipError_t launch_append(const AppendArgs& a, int cus, hipStream_t stream) {
     // 32 teams in flight per CU's worth of blocks; teams stride over datagrams
     const uint32_t want = (a.n + (kThreads / kTeam) - 1) / (kThreads / kTeam);
-    const uint32_t cap = (uint32_t)cus * 16u;
+    const uint32_t cap = (uint32_t)cus * LNL_APPEND_WGS;
     const uint32_t grid = want < cap ? want : cap;
     hipLaunchKernelGGL(append_kernel, dim3(grid ? grid : 1), dim3(kThreads), 0, stream, a);
     return hipGetLastError();

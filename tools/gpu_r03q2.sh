@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${1:-r03q2}
+timeout -k 10 300 python -u tools/kvariants.py run --names base,app_w4,app_w8,app_w32 --rounds 8 --workloads append:1048576:64:1400 --out gpurun_out/${TAG}_kv.json > gpurun_out/${TAG}_kv.log 2>&1 || { tail -20 gpurun_out/${TAG}_kv.log; exit 1; }
+cat gpurun_out/${TAG}_kv.log

@@ -36,6 +36,9 @@ VARIANTS = {
     "app_nts": "-DLNL_APPEND_NT=1",                 # append kernel: nontemporal chunk stores
     "app_ntl": "-DLNL_APPEND_NT=2",                 # ... loads
     "app_nt": "-DLNL_APPEND_NT=3",                  # ... both
+    "app_w4": "-DLNL_APPEND_WGS=4u",                # append kernel: 4 / 8 / 32 workgroups per CU (default 16)
+    "app_w8": "-DLNL_APPEND_WGS=8u",
+    "app_w32": "-DLNL_APPEND_WGS=32u",
     "app_nohead": "-DLNL_APPEND_DIAG=1",            # append kernel: no head / tail byte stores (wrong burst)
     "app_nochunk": "-DLNL_APPEND_DIAG=2",           # ... no chunk stores (wrong burst)
     "app_nostore": "-DLNL_APPEND_DIAG=3",           # ... no stores at all (wrong burst)
