@@ -52,7 +52,11 @@ using namespace dev;
 #define LNL_RUN_PRIO 0
 #endif
 constexpr int kWaves = kRunThreads / 64;
-constexpr int kLdsU4 = kWaves * 2 * kBufU4 + kFoldU4 + 1;  // + one uint4: per-wave progress words
+constexpr int kBufsU4 = kWaves * 2 * kBufU4;  // the waves' row buffers
+constexpr int kFoldLdsU4 = kFoldU4 + 1;       // the tables + one uint4: per-wave progress words
+#ifndef LNL_RUN_EARLY_ROWS
+#define LNL_RUN_EARLY_ROWS 1  // first rows issued before the tables land (0: after, as before round 3)
+#endif
 static_assert(!LNL_RUN_PRIO || kWaves == 8, "priority balancing pairs wave w with w ^ 4");
 
 // Wave-uniform description of one lane-run batch.
@@ -141,25 +145,23 @@ __device__ LNL_INLINE uint32_t final_map(uint32_t fold_base, uint32_t e, uint32_
 }
 
 __global__ __launch_bounds__(kRunThreads, 512 / kRunThreads) void crc32c_run_kernel(RunArgs a) {
-    __shared__ __attribute__((aligned(16))) uint4 lds[kLdsU4];
+    // row buffers and tables in separate LDS arrays: the tables' LDS writes
+    // then provably do not touch the LDS-DMA destinations, and the wait before
+    // them can leave the first rows in flight
+    __shared__ __attribute__((aligned(128))) uint4 bufs[kBufsU4];
+    __shared__ __attribute__((aligned(16))) uint4 fold_arr[kFoldLdsU4];
     const uint32_t lane = __lane_id();
     const uint32_t wave = uni(threadIdx.x >> 6);
-    uint4* const buf_base = lds + wave * (2 * kBufU4);
-    uint4* const fold_lds = lds + kWaves * 2 * kBufU4;
+    uint4* const buf_base = bufs + wave * (2 * kBufU4);
+    uint4* const fold_lds = fold_arr;
     const uint32_t fold_base = (uint32_t)(uintptr_t)fold_lds;
-    {
-        const uint4* g = reinterpret_cast<const uint4*>(a.fold);
-        for (int i = threadIdx.x; i < kFoldU4; i += kRunThreads) fold_lds[i] = g[i];
-        if (threadIdx.x == 0) fold_lds[kFoldU4] = make_uint4(0u, 0u, 0u, 0u);
-        __syncthreads();
-    }
     uint32_t* const prog = reinterpret_cast<uint32_t*>(fold_lds + kFoldU4);
     uint32_t rows_done = 0;
     (void)prog;
     (void)rows_done;
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint32_t nw = gridDim.x * kWaves;
-    if (gw >= a.nb) return;
+    const bool active = gw < a.nb;
 
     uint32_t off[2];
     const uint32_t qs8 = 8u * a.q * (uint32_t)a.stride;
@@ -176,12 +178,54 @@ __global__ __launch_bounds__(kRunThreads, 512 / kRunThreads) void crc32c_run_ker
     const bool contiguous = S == L;
 
     uint32_t wb = gw;
-    RunBatch cur = run_batch(a, wb), nxt{};
-    bool has_nxt = wb + nw < a.nb;
-    if (has_nxt) nxt = run_batch(a, wb + nw);
-    // rows >= 2 always (len >= 129)
-    issue_run_row(cur, 0, off, qs8, buf_base);
-    issue_run_row(cur, 1, off, qs8, buf_base + kBufU4);
+    RunBatch cur{}, nxt{};
+    bool has_nxt = false;
+    // The tables' loads go out first, then this wave's first two rows (rows >= 2
+    // always: len >= 129), then the tables go to LDS: the wait before those LDS
+    // writes counts the 16 row loads issued after them, so the rows stream
+    // while the tables land (before round 3 the rows waited for the tables).
+    {
+        constexpr int kPer = (kFoldU4 + kRunThreads - 1) / kRunThreads;
+        u32x4 tv[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {  // (inline asm: the compiler inserts no wait for them)
+            const int i = (int)threadIdx.x + j * kRunThreads;
+            const uint64_t at = (uint64_t)(uintptr_t)a.fold + 16u * (uint32_t)(i < kFoldU4 ? i : kFoldU4 - 1);
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(tv[j]) : "v"(at) : "memory");
+        }
+        auto first_rows = [&]() {
+            if (!active) return;
+            cur = run_batch(a, wb);
+            has_nxt = wb + nw < a.nb;
+            if (has_nxt) nxt = run_batch(a, wb + nw);
+            issue_run_row(cur, 0, off, qs8, buf_base);
+            issue_run_row(cur, 1, off, qs8, buf_base + kBufU4);
+        };
+#if LNL_RUN_EARLY_ROWS
+        first_rows();
+        if (active)
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the tables only
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = (int)threadIdx.x + j * kRunThreads;
+            asm volatile("" : "+v"(tv[j]));
+            if (i < kFoldU4) lds_write_piece(fold_base + 16u * (uint32_t)i, tv[j]);
+        }
+        if (threadIdx.x == 0) lds_write_piece(fold_base + 16u * (uint32_t)kFoldU4, u32x4{0u, 0u, 0u, 0u});
+        // the tables are in LDS (lgkmcnt) before the barrier; a plain s_barrier,
+        // not __syncthreads, whose fence would also wait for the rows in flight
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#if !LNL_RUN_EARLY_ROWS
+        first_rows();
+#endif
+    }
+    if (!active) return;
 
     uint32_t s[32], P[32];
 #pragma unroll

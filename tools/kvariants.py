@@ -75,6 +75,7 @@ VARIANTS = {
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
     "k16": "-DLNL_RUN_K=16",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
+    "run_late": "-DLNL_RUN_EARLY_ROWS=0",           # run kernel: first rows issued after the tables land (before round 3)
     # CSR experiment paths: same library, runtime path (lnl_crc32c_set_csr_path)
     "uniform": ("", 1),                             # CSR: uniform line-count batches, shared lines once
     "seg": ("", 2),                                 # CSR: segment kernel
