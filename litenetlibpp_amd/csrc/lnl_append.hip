@@ -29,6 +29,12 @@ constexpr int kThreads = 256;
 #define LNL_APPEND_TEAM 32  // measured: 16 lanes 559 us, 32 lanes 512 us, 64 lanes 613 us per config-3 call
 #endif
 constexpr uint32_t kTeam = LNL_APPEND_TEAM;  // lanes per datagram
+#ifndef LNL_APPEND_STORE_SFX
+#define LNL_APPEND_STORE_SFX ""  // chunk stores' cache-policy suffix.  The asm store itself is the gain
+                                // (489-493 us against 502 us for the C store: the loop is not unrolled
+                                // and the wave reaches its next loads sooner); sc0 is no faster than the
+                                // default, sc1 / sc0 sc1 / nt are 15-17 % slower
+#endif
 #ifndef LNL_APPEND_WGS
 #define LNL_APPEND_WGS 16u  // workgroups per CU (teams stride over the datagrams)
 #endif
@@ -87,7 +93,6 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
         const uint8_t v0 = b0 ? out_byte(x0, P1, delta, crc) : 0;
         const uint8_t v1 = b1 ? out_byte(x1, P1, delta, crc) : 0;
         const uint32_t c = (uint32_t)((c0 - delta) & 3u);  // (the same for every chunk)
-#pragma unroll 2
         for (uint64_t w = c0 + 16ull * q; w < c1; w += 16ull * kTeam) {
             const uint64_t sw = (w - delta) & ~(uint64_t)3;
 #if LNL_APPEND_NT & 2
@@ -108,8 +113,10 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
             if (w == 7u) *LNL_G(uint4, w) = o;  // diagnostic build only: no chunk stores (wrong burst)
 #elif LNL_APPEND_NT & 1
             __builtin_nontemporal_store(dev::u32x4{o.x, o.y, o.z, o.w}, LNL_G(dev::u32x4, w));
-#else
-            *LNL_G(uint4, w) = o;
+#else  // cache-policy suffix (LNL_APPEND_STORE_SFX; "" for the default policy)
+            asm volatile("global_store_dwordx4 %0, %1, off " LNL_APPEND_STORE_SFX ::"v"(w),
+                         "v"(dev::u32x4{o.x, o.y, o.z, o.w})
+                         : "memory");
 #endif
         }
 #if defined(LNL_APPEND_DIAG) && (LNL_APPEND_DIAG & 1)

@@ -36,6 +36,10 @@ VARIANTS = {
     "app_nts": "-DLNL_APPEND_NT=1",                 # append kernel: nontemporal chunk stores
     "app_ntl": "-DLNL_APPEND_NT=2",                 # ... loads
     "app_nt": "-DLNL_APPEND_NT=3",                  # ... both
+    "app_scdf": "-DLNL_APPEND_STORE_SFX=\\\"\\\"",   # append kernel: chunk stores with the default policy (the product)
+    "app_sc1": "-DLNL_APPEND_STORE_SFX=\\\"sc1\\\"",   # append kernel: chunk stores with cache-policy bits
+    "app_sc01": "-DLNL_APPEND_STORE_SFX=\\\"sc0\\ sc1\\\"",
+    "app_sc0": "-DLNL_APPEND_STORE_SFX=\\\"sc0\\\"",
     "app_w4": "-DLNL_APPEND_WGS=4u",                # append kernel: 4 / 8 / 32 workgroups per CU (default 16)
     "app_w8": "-DLNL_APPEND_WGS=8u",
     "app_w32": "-DLNL_APPEND_WGS=32u",
