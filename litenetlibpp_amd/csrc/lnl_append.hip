@@ -93,6 +93,9 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
         const uint8_t v0 = b0 ? out_byte(x0, P1, delta, crc) : 0;
         const uint8_t v1 = b1 ? out_byte(x1, P1, delta, crc) : 0;
         const uint32_t c = (uint32_t)((c0 - delta) & 3u);  // (the same for every chunk)
+#if defined(LNL_APPEND_UNROLL) && LNL_APPEND_UNROLL == 2  // experiments
+#pragma unroll 2
+#endif
         for (uint64_t w = c0 + 16ull * q; w < c1; w += 16ull * kTeam) {
             const uint64_t sw = (w - delta) & ~(uint64_t)3;
 #if LNL_APPEND_NT & 2
