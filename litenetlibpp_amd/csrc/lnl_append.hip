@@ -60,20 +60,28 @@ __global__ __launch_bounds__(kThreads) void append_kernel(AppendArgs a) {
     const uint64_t o0 = a.off[0];
     const uint64_t dstb = (uint64_t)(uintptr_t)a.dst, srcb = (uint64_t)(uintptr_t)a.base - a.off0;
     // the next datagram's offsets and CRC are fetched one datagram ahead
+#if defined(LNL_APPEND_BLOCKED) && LNL_APPEND_BLOCKED  // experiments: team t owns a run of consecutive datagrams
+    const uint32_t per = (a.n + nt - 1) / nt;
+    const uint64_t i0 = (uint64_t)t * per, iend = i0 + per < a.n ? i0 + per : a.n;
+    const uint32_t step = 1;
+#else  // the product: teams stride over the datagrams, so the burst is written as one front
+    const uint64_t i0 = t, iend = a.n;
+    const uint32_t step = nt;
+#endif
     uint64_t ns = 0, ne = 0;
     uint32_t ncrc = 0;
-    if (t < a.n) {
-        ns = a.off[t];
-        ne = a.off[t + 1];
-        ncrc = a.crc[t];
+    if (i0 < iend) {
+        ns = a.off[i0];
+        ne = a.off[i0 + 1];
+        ncrc = a.crc[i0];
     }
-    for (uint32_t i = t; i < a.n; i += nt) {
+    for (uint32_t i = (uint32_t)i0; i < iend; i += step) {
         const uint64_t s = ns, e = ne;
         const uint32_t crc = ncrc;
-        if (i + nt < a.n) {
-            ns = a.off[i + nt];
-            ne = a.off[i + nt + 1];
-            ncrc = a.crc[i + nt];
+        if (i + step < iend) {
+            ns = a.off[i + step];
+            ne = a.off[i + step + 1];
+            ncrc = a.crc[i + step];
         }
         const uint64_t P0 = dstb + (s - o0) + 4ull * i;  // first payload byte in dst
         const uint64_t P1 = P0 + (e - s);                // first CRC byte

@@ -38,6 +38,7 @@ VARIANTS = {
     "app_nt": "-DLNL_APPEND_NT=3",                  # ... both
     "app_scdf": "-DLNL_APPEND_STORE_SFX=\\\"\\\"",   # append kernel: chunk stores with the default policy (the product)
     "app_u2": "-DLNL_APPEND_UNROLL=2",   # append kernel: the chunk loop unrolled twice around the asm store
+    "app_blk": "-DLNL_APPEND_BLOCKED=1",   # append kernel: each team owns a run of consecutive datagrams
     "app_sc1": "-DLNL_APPEND_STORE_SFX=\\\"sc1\\\"",   # append kernel: chunk stores with cache-policy bits
     "app_sc01": "-DLNL_APPEND_STORE_SFX=\\\"sc0\\ sc1\\\"",
     "app_sc0": "-DLNL_APPEND_STORE_SFX=\\\"sc0\\\"",
