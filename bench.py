@@ -32,7 +32,8 @@ on this host over the WHOLE batch (copied to host memory, untimed), on one
 core and on every core this process may run on (rank 0, N = 1); the checker
 also compares the GPU's output for the whole batch with it.
 host_path: config 5 -- the same batch from pinned host memory through
-lnl_crc32c_batch_host (H2D + kernel + D2H on 4 streams), PCIe-inclusive.
+lnl_crc32c_batch_host_ex (H2D + kernel + D2H on 2 HIP streams, BASELINE
+configs[4]; the 4-stream default beside it), PCIe-inclusive.
 """
 from __future__ import annotations
 
@@ -85,6 +86,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the config-5 (PCIe-inclusive) measurement")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise torch.distributed (backend nccl = RCCL on the GPU box) even at --gpus 1 and "
+                         "run every collective the N-rank path runs (barrier with device_ids, MAX / SUM / gather "
+                         "on device tensors, destroy_process_group): a one-GPU rehearsal of the driver's "
+                         "multi-GPU run (DESIGN 6)")
     return ap.parse_args()
 
 
@@ -400,46 +406,55 @@ def parity_sample(w, out, host):
     return ok, k
 
 
+def _host_timed(fn, reps=3):
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        got = fn()
+    return (time.perf_counter() - t0) / reps, got
+
+
 def host_path_rate(P, host, w, device):
-    """Config 5: host-resident pinned batch -> lnl_crc32c_batch_host (H2D +
-    kernel + D2H over 4 streams).  PCIe-inclusive; never the headline value."""
+    """Config 5: host-resident pinned batch -> lnl_crc32c_batch_host_ex on 2
+    HIP streams (BASELINE.json configs[4]), H2D + kernel + D2H, chunks of 64 Ki
+    datagrams; the library's default (4 streams) beside it.  PCIe-inclusive;
+    never the headline value."""
     data, off = host
     if off is None:
         off = np.arange(0, (w["n"] + 1) * w["L"], w["L"], dtype=np.uint64)
     pinned = torch.from_numpy(data).pin_memory().numpy()
-    P.batch_host(pinned, off, device)
     reps = 3
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        got = P.batch_host(pinned, off, device)
-    dt = (time.perf_counter() - t0) / reps
-    return {"value": round(w["payload"] / dt / 1e9, 2), "unit": "GB/s",
-            "what": "config 5: the same batch in pinned host memory through lnl_crc32c_batch_host "
-                    "(H2D + kernel + D2H, 4 streams, chunks of <= 64 Ki datagrams / 64 MiB), blocking, "
-                    f"mean of {reps} calls"}, got
+    dt2, got = _host_timed(lambda: P.batch_host(pinned, off, device, streams=2), reps)
+    dt4, got4 = _host_timed(lambda: P.batch_host(pinned, off, device, streams=4), reps)
+    return {"value": round(w["payload"] / dt2 / 1e9, 2), "unit": "GB/s", "streams": 2,
+            "value_4_streams": round(w["payload"] / dt4 / 1e9, 2),
+            "what": "config 5: the same batch in pinned host memory through lnl_crc32c_batch_host_ex "
+                    "(H2D + kernel + D2H overlapped on 2 HIP streams, chunks of <= 64 Ki datagrams / 64 MiB), "
+                    f"blocking, mean of {reps} calls; value_4_streams: the library default, 4 streams",
+            "parity_4_streams": "equal to the 2-stream output" if np.array_equal(got, got4) else "MISMATCH"}, got
 
 
 def host_append_rate(P, host, w, device):
     """The send side from host memory: the same payload burst, pinned, through
-    lnl_crc32c_append_host (H2D + CRC + append + D2H of the wire burst, 2
-    streams), PCIe-inclusive; the wire bytes of the first datagrams checked
-    against the device-resident call's."""
+    lnl_crc32c_append_host_ex (H2D + CRC + append + D2H of the wire burst) on
+    2 HIP streams (config 5's count) and on 4 (the library default: the D2H of
+    a chunk no longer holds up its stream's next H2D), PCIe-inclusive; the
+    wire bytes of the first datagrams checked against the device-resident
+    call's."""
     data, off = host
     pinned = torch.from_numpy(data).pin_memory().numpy()
     out = torch.empty(int(off[-1] - off[0]) + 4 * w["n"], dtype=torch.uint8).pin_memory().numpy()
-    wire, woff = P.append_host(pinned, off, device, out=out)
     reps = 3
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        P.append_host(pinned, off, device, out=out)
-    dt = (time.perf_counter() - t0) / reps
+    dt2, (wire, woff) = _host_timed(lambda: P.append_host(pinned, off, device, out=out, streams=2), reps)
     k = min(w["n"], 1 << 14)
     ok = np.array_equal(wire[: int(woff[k])], w["wire"][: int(woff[k])].cpu().numpy())
-    return {"value": round(w["payload"] / dt / 1e9, 2), "unit": "GB/s",
-            "what": "the payload burst in pinned host memory through lnl_crc32c_append_host (H2D payload + "
-                    "offsets, CRC + append, D2H of the wire burst into pinned memory; 4 streams), blocking, "
-                    "payload bytes / time, "
-                    f"mean of {reps} calls",
+    dt4, (wire4, _) = _host_timed(lambda: P.append_host(pinned, off, device, out=out, streams=4), reps)
+    ok = ok and np.array_equal(wire4[: int(woff[k])], w["wire"][: int(woff[k])].cpu().numpy())
+    return {"value": round(w["payload"] / dt2 / 1e9, 2), "unit": "GB/s", "streams": 2,
+            "value_4_streams": round(w["payload"] / dt4 / 1e9, 2),
+            "what": "the payload burst in pinned host memory through lnl_crc32c_append_host_ex (H2D payload + "
+                    "offsets, CRC + append, D2H of the wire burst into pinned memory) on 2 HIP streams, "
+                    f"blocking, payload bytes / time, mean of {reps} calls; value_4_streams: 4 streams",
             "parity": "wire bytes equal the device-resident call's" if ok else "MISMATCH"}
 
 
@@ -467,8 +482,11 @@ def main():
         torch.cuda.set_device(gpu)
         device = torch.device("cuda", gpu)
     red_dev = device if backend == "nccl" else None
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
         # bounded rendezvous: a rank that never arrives ends the run, not hangs it
         tmo = datetime.timedelta(seconds=300)
         if backend == "nccl":
@@ -480,7 +498,7 @@ def main():
         P.lib()
 
     def barrier():
-        if world > 1:
+        if dist_on:
             dist.barrier(device_ids=[gpu]) if backend == "nccl" else dist.barrier()
 
     def sync():
@@ -621,6 +639,10 @@ def main():
                 "kernel_ms_per_rank": [round(k, 5) for k in kern_all],
             },
         }
+        line["distributed"] = ({"backend": backend, "world_size": world, "forced": bool(args.force_dist and world == 1),
+                                "collectives": "barrier(device_ids), all_reduce MAX/SUM, all_gather on "
+                                               + ("device tensors" if red_dev is not None else "CPU tensors")}
+                               if dist_on else None)
         if DRY:
             line["dry_run"] = "LNL_BENCH_DRYRUN=1: CPU plumbing test, no kernel ran; figures are meaningless"
         if "line_bytes" in w:  # random narrow reads: HBM moves whole 64-B sectors
@@ -676,7 +698,7 @@ def main():
                 got, out.cpu().numpy().view(np.uint32)) else "MISMATCH"
             line["host_path"] = hp
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

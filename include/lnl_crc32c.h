@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 8
+#define LNL_CRC32C_ABI_VERSION 9
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -130,7 +130,8 @@ int lnl_inbound_filter_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uin
                                uint8_t* d_status, void* hip_stream);
 
 /* Host-resident batch (the socket path): copies h_base/h_off to `device`
- * in chunks over four HIP streams (H2D -> kernel -> D2H overlapped), writes
+ * in chunks over LNL_HOST_DEFAULT_STREAMS HIP streams (H2D -> kernel -> D2H
+ * overlapped; lnl_crc32c_batch_host_ex below sets the count), writes
  * h_out[i], blocks until done.  h_off as in batch_csr_dev (h_off[0] may be
  * nonzero).  Pinned (hipHostMalloc / hipHostRegister) buffers give the full
  * PCIe rate; pageable ones work but copy through a staging buffer. */
@@ -174,7 +175,7 @@ int lnl_xor_layer_fixed_dev(uint8_t* d_base, size_t stride, uint32_t len, uint32
                             size_t key_len, void* hip_stream);
 
 /* Host-resident inbound filter (lnl_inbound_filter_csr_dev over a pinned host
- * burst, same chunked two-stream pipeline as lnl_crc32c_batch_host): writes
+ * burst, the same chunked pipeline as lnl_crc32c_batch_host): writes
  * h_status[i] (LNL_INBOUND_*), blocks until done. */
 int lnl_inbound_filter_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                             uint8_t* h_status, int device);
@@ -217,9 +218,10 @@ int lnl_crc32c_append_host(const uint8_t* h_payload, const uint64_t* h_off, uint
  * connected socket, else naddrs (1: one endpoint for all, or n: one per
  * datagram) struct sockaddr_in.  status (optional, n entries) receives, for
  * every datagram attempted, the bytes sent or a negative errno for a datagram
- * the kernel refused (send_raw's error case, :525-567; the burst goes on).
- * When the socket buffer is full, wait_ms != 0 polls for room (-1: forever)
- * and 0 returns at once.  Returns the number of datagrams attempted, from the
+ * the kernel refused (send_raw's error case, :525-567, ENOBUFS included; the
+ * burst goes on).  When the socket buffer is full (EAGAIN), wait_ms > 0 polls
+ * for room until one deadline wait_ms after the call started, -1 polls
+ * without a deadline, and 0 returns at once.  Returns the number of datagrams attempted, from the
  * front (the rest were not: buffer full and the wait expired), or a negative
  * errno when the call itself is invalid (bad fd, arguments). */
 int64_t lnl_egress_send_batch(int fd, const uint8_t* wire, const uint64_t* off, uint32_t n, const void* addrs,
@@ -236,7 +238,59 @@ int64_t lnl_egress_send_batch(int fd, const uint8_t* wire, const uint64_t* off, 
 int lnl_crc32c_batch_host_multi(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                                 uint32_t* h_out, const int* devices, int ndev);
 
+/* ---- host pipelines with explicit options -------------------------------- */
+
+/* Options of the host-resident pipelines (lnl_crc32c_batch_host,
+ * lnl_inbound_filter_host, lnl_crc32c_append_host take the defaults).  A zero
+ * field takes its default; `size` must be sizeof(lnl_host_opts) (a larger
+ * struct from a newer header is accepted, its extra fields ignored).
+ *   streams          HIP streams the chunks go round-robin over, each with its
+ *                    own device staging slot: 1 .. LNL_HOST_MAX_STREAMS
+ *                    (default LNL_HOST_DEFAULT_STREAMS).  Two is BASELINE
+ *                    config 5 ("overlapped on 2 HIP streams"); with two, a
+ *                    stream's next H2D waits behind its own D2H, which costs
+ *                    the send side (a D2H as large as its H2D), not the CRC
+ *                    and filter paths.
+ *   chunk_datagrams  datagrams per chunk at most (default 65536)
+ *   chunk_bytes      bytes per chunk at most (default 64 MiB; a single longer
+ *                    datagram gets a chunk of its own) */
+#define LNL_HOST_MAX_STREAMS 8
+#define LNL_HOST_DEFAULT_STREAMS 4
+typedef struct lnl_host_opts {
+    uint32_t size;
+    uint32_t streams;
+    uint32_t chunk_datagrams;
+    uint32_t reserved; /* 0 */
+    uint64_t chunk_bytes;
+} lnl_host_opts;
+
+/* lnl_crc32c_batch_host / lnl_inbound_filter_host / lnl_crc32c_append_host
+ * with options (opts may be NULL: every default).  -EINVAL for a bad size,
+ * streams > LNL_HOST_MAX_STREAMS or a nonzero reserved field. */
+int lnl_crc32c_batch_host_ex(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, uint32_t* h_out,
+                             int device, const lnl_host_opts* opts);
+int lnl_inbound_filter_host_ex(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, uint8_t* h_status,
+                               int device, const lnl_host_opts* opts);
+int lnl_crc32c_append_host_ex(const uint8_t* h_payload, const uint64_t* h_off, uint32_t n, uint8_t* h_wire,
+                              uint32_t* h_crc, int device, const lnl_host_opts* opts);
+
 /* ---- misc ---------------------------------------------------------------- */
+
+/* Releases the device scratch the library keeps for `hip_stream` on the
+ * current device (the CSR span path's control and exchange blocks, the XOR
+ * chunk map), stream-ordered.  Call it before destroying a stream the batch
+ * entry points were given; the library also bounds what it keeps (the least
+ * recently used streams' scratch is freed beyond LNL_STREAM_CACHE per device).
+ * Returns 0 (also when nothing was kept for the stream). */
+#define LNL_STREAM_CACHE 32
+int lnl_stream_release(void* hip_stream);
+
+/* Diagnostics (tests): fills every wave-batch exchange arrival word of the span
+ * scratch kept for `hip_stream` with `value`, as an aborted call could leave
+ * it.  Synchronises the stream first; blocking.  -ENOENT when no CSR call has
+ * run on the stream yet.  Later calls must be unaffected (the arrival words
+ * pair by per-call epoch, crc32c_span.h). */
+int lnl_diag_fill_span_arrivals(void* hip_stream, uint64_t value);
 
 /* Message for the last failure on the calling thread ("" if none). */
 const char* lnl_crc32c_last_error(void);

@@ -33,7 +33,10 @@ from .crc32c import (  # noqa: F401
     crc32c_extend,
     mtu_with_layer,
     verify_csr,
+    stream_release,
+    HOST_DEFAULT_STREAMS,
+    HOST_MAX_STREAMS,
 )
-from ._lib import LIB_PATH, lib  # noqa: F401
+from ._lib import LIB_PATH, HostOpts, lib  # noqa: F401
 
 __version__ = "0.1.0"

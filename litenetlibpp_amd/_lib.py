@@ -24,6 +24,19 @@ class Crc32cError(RuntimeError):
         self.code = code
 
 
+class HostOpts(ctypes.Structure):
+    """struct lnl_host_opts (include/lnl_crc32c.h): zero fields take the defaults."""
+    _fields_ = [("size", ctypes.c_uint32), ("streams", ctypes.c_uint32), ("chunk_datagrams", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint64)]
+
+    @classmethod
+    def make(cls, streams: int = 0, chunk_datagrams: int = 0, chunk_bytes: int = 0) -> "HostOpts":
+        return cls(ctypes.sizeof(cls), streams, chunk_datagrams, 0, chunk_bytes)
+
+
+HOST_MAX_STREAMS = 8       # LNL_HOST_MAX_STREAMS
+HOST_DEFAULT_STREAMS = 4   # LNL_HOST_DEFAULT_STREAMS
+
 _lib = None
 
 
@@ -89,6 +102,17 @@ def lib() -> ctypes.CDLL:
     L.lnl_xor_layer_fixed_dev.restype = ctypes.c_int
     L.lnl_xor_layer_fixed_dev.argtypes = [_c_u8p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _c_u8p,
                                           ctypes.c_size_t, ctypes.c_void_p]
+    opts_p = ctypes.POINTER(HostOpts)
+    L.lnl_crc32c_batch_host_ex.restype = ctypes.c_int
+    L.lnl_crc32c_batch_host_ex.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, ctypes.c_int, opts_p]
+    L.lnl_inbound_filter_host_ex.restype = ctypes.c_int
+    L.lnl_inbound_filter_host_ex.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, ctypes.c_int, opts_p]
+    L.lnl_crc32c_append_host_ex.restype = ctypes.c_int
+    L.lnl_crc32c_append_host_ex.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, ctypes.c_int, opts_p]
+    L.lnl_stream_release.restype = ctypes.c_int
+    L.lnl_stream_release.argtypes = [ctypes.c_void_p]
+    L.lnl_diag_fill_span_arrivals.restype = ctypes.c_int
+    L.lnl_diag_fill_span_arrivals.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     L.lnl_crc32c_last_error.restype = ctypes.c_char_p
     L.lnl_crc32c_last_error.argtypes = []
     L.lnl_crc32c_abi_version.restype = ctypes.c_int

@@ -26,7 +26,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import Crc32cError, check, lib
+from ._lib import HOST_DEFAULT_STREAMS, HOST_MAX_STREAMS, Crc32cError, HostOpts, check, lib
 
 EXTRA_PACKET_SIZE = 4  # LNL_CRC32C_LAYER_EXTRA / upstream ExtraPacketSizeForLayer
 HEADER_SIZE = 1        # net_constants::HEADER_SIZE (/root/reference/include/lnl/net_constants.h:16)
@@ -36,7 +36,7 @@ __all__ = [
     "batch_fixed", "batch_csr", "verify_csr", "batch_host", "batch_host_multi", "mtu_with_layer",
     "packet_verify", "inbound_status", "inbound_filter", "filter_dispatch", "inbound_filter_host", "ingress_recv_batch",
     "dispatch", "xor_layer", "xor_layer_csr", "xor_layer_fixed",
-    "INGRESS_SLOT",
+    "INGRESS_SLOT", "HOST_DEFAULT_STREAMS", "HOST_MAX_STREAMS", "stream_release",
     "INBOUND_DROP_CRC", "INBOUND_ACCEPT", "INBOUND_MALFORMED",
 ]
 
@@ -367,15 +367,27 @@ def _host_csr(data, offsets):
     return data, off
 
 
-def inbound_filter_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
+def _host_opts(streams, chunk_datagrams, chunk_bytes):
+    """ctypes pointer to an lnl_host_opts (None: every default)."""
+    if not (streams or chunk_datagrams or chunk_bytes):
+        return None
+    if streams and not 1 <= streams <= HOST_MAX_STREAMS:
+        raise ValueError(f"streams must be 1..{HOST_MAX_STREAMS}")
+    return ctypes.pointer(HostOpts.make(streams or 0, chunk_datagrams or 0, chunk_bytes or 0))
+
+
+def inbound_filter_host(data: np.ndarray, offsets: np.ndarray, device: int = 0, streams: Optional[int] = None,
+                        chunk_datagrams: Optional[int] = None, chunk_bytes: Optional[int] = None) -> np.ndarray:
     """Host-resident burst through the GPU inbound filter (H2D -> filter ->
-    D2H on 4 streams).  Blocking.  Returns uint8 status codes."""
+    D2H, chunks over ``streams`` HIP streams, default HOST_DEFAULT_STREAMS).
+    Blocking.  Returns uint8 status codes.  Mirrors lnl_inbound_filter_host_ex."""
     data, offsets = _host_csr(data, offsets)
+    opts = _host_opts(streams, chunk_datagrams, chunk_bytes)
     n = offsets.size - 1
     out = np.empty(max(n, 0), dtype=np.uint8)
     if n > 0:
-        check(lib().lnl_inbound_filter_host(data.ctypes.data, offsets.ctypes.data, n, out.ctypes.data, device),
-              "lnl_inbound_filter_host")
+        check(lib().lnl_inbound_filter_host_ex(data.ctypes.data, offsets.ctypes.data, n, out.ctypes.data, device,
+                                               opts), "lnl_inbound_filter_host_ex")
     return out
 
 
@@ -394,15 +406,18 @@ def ingress_recv_batch(fd: int, buf: np.ndarray, max_n: int, wait_ms: int = 0):
     return r, off[: r + 1]
 
 
-def append_host(data: np.ndarray, offsets: np.ndarray, device: int = 0, want_crc: bool = False, out=None):
-    """Host-resident outbound layer over the GPU (H2D -> CRC + append -> D2H on
-    2 streams).  Blocking.  Returns (wire, wire_offsets[, crc]): datagram i is
+def append_host(data: np.ndarray, offsets: np.ndarray, device: int = 0, want_crc: bool = False, out=None,
+                streams: Optional[int] = None, chunk_datagrams: Optional[int] = None,
+                chunk_bytes: Optional[int] = None):
+    """Host-resident outbound layer over the GPU (H2D -> CRC + append -> D2H,
+    chunks over ``streams`` HIP streams, default HOST_DEFAULT_STREAMS).  Blocking.  Returns (wire, wire_offsets[, crc]): datagram i is
     wire[wire_offsets[i] .. wire_offsets[i + 1]) = payload || LE32(CRC), the
     bytes Crc32cLayer.process_outbound gives for it.  ``out``: a uint8 array of
     at least the wire burst's size to write it into -- pinned memory (as for
     ``data``) gives the full PCIe rate; a fresh pageable array otherwise.
-    Mirrors lnl_crc32c_append_host."""
+    Mirrors lnl_crc32c_append_host_ex."""
     data, offsets = _host_csr(data, offsets)
+    opts = _host_opts(streams, chunk_datagrams, chunk_bytes)
     n = offsets.size - 1
     wire_off = (offsets - offsets[0]) + EXTRA_PACKET_SIZE * np.arange(n + 1, dtype=np.uint64)
     if out is not None:
@@ -413,9 +428,9 @@ def append_host(data: np.ndarray, offsets: np.ndarray, device: int = 0, want_crc
         wire = np.empty(int(wire_off[-1]), dtype=np.uint8)
     crc = np.empty(max(n, 0), dtype=np.uint32) if want_crc else None
     if n > 0:
-        check(lib().lnl_crc32c_append_host(data.ctypes.data, offsets.ctypes.data, n, wire.ctypes.data,
-                                           None if crc is None else crc.ctypes.data, device),
-              "lnl_crc32c_append_host")
+        check(lib().lnl_crc32c_append_host_ex(data.ctypes.data, offsets.ctypes.data, n, wire.ctypes.data,
+                                              None if crc is None else crc.ctypes.data, device, opts),
+              "lnl_crc32c_append_host_ex")
     return (wire, wire_off, crc) if want_crc else (wire, wire_off)
 
 
@@ -450,16 +465,27 @@ def egress_send_batch(fd: int, wire: np.ndarray, offsets: np.ndarray, addrs=None
     return int(r), status
 
 
-def batch_host(data: np.ndarray, offsets: np.ndarray, device: int = 0) -> np.ndarray:
-    """Host-resident batch over the GPU (H2D -> kernel -> D2H on 2 streams).
-    Blocking.  ``data`` uint8, ``offsets`` uint64/int64 with n+1 entries."""
+def batch_host(data: np.ndarray, offsets: np.ndarray, device: int = 0, streams: Optional[int] = None,
+               chunk_datagrams: Optional[int] = None, chunk_bytes: Optional[int] = None) -> np.ndarray:
+    """Host-resident batch over the GPU (H2D -> kernel -> D2H, chunks over
+    ``streams`` HIP streams, default HOST_DEFAULT_STREAMS; BASELINE config 5 is
+    streams=2).  Blocking.  ``data`` uint8, ``offsets`` uint64/int64 with n+1
+    entries.  Mirrors lnl_crc32c_batch_host_ex."""
     data, offsets = _host_csr(data, offsets)
+    opts = _host_opts(streams, chunk_datagrams, chunk_bytes)
     n = offsets.size - 1
     out = np.empty(max(n, 0), dtype=np.uint32)
     if n > 0:
-        check(lib().lnl_crc32c_batch_host(data.ctypes.data, offsets.ctypes.data, n, out.ctypes.data,
-                                          device), "lnl_crc32c_batch_host")
+        check(lib().lnl_crc32c_batch_host_ex(data.ctypes.data, offsets.ctypes.data, n, out.ctypes.data,
+                                             device, opts), "lnl_crc32c_batch_host_ex")
     return out
+
+
+def stream_release(stream=None) -> None:
+    """Frees the scratch the library keeps for ``stream`` (a torch stream,
+    a raw hipStream_t handle or None) on the current device; call it before
+    the stream goes away.  Mirrors lnl_stream_release."""
+    lib().lnl_stream_release(stream if isinstance(stream, int) else _stream_handle(stream))
 
 
 def batch_host_multi(data: np.ndarray, offsets: np.ndarray, devices) -> np.ndarray:

@@ -54,15 +54,23 @@ int hip_fail(hipError_t e, const char* what) {
 constexpr int kMaxDevices = 64;
 
 // Host paths (lnl_crc32c_batch_host, lnl_inbound_filter_host,
-// lnl_crc32c_append_host): chunks go round-robin over this many streams, each
-// with its own staging buffers.  With two, a stream's next H2D waits behind its
+// lnl_crc32c_append_host and their _ex forms): chunks go round-robin over
+// `streams` streams (lnl_host_opts; LNL_HOST_DEFAULT_STREAMS by default), each
+// with its own staging slot.  With two, a stream's next H2D waits behind its
 // own D2H, so the send side (a D2H as large as its H2D) overlapped the two
 // directions only half the time; from three on, the H2D of chunk k + 1 .. k + 3
 // runs while chunk k's wire burst comes back.
-#ifndef LNL_HOST_SLOTS
-#define LNL_HOST_SLOTS 4
-#endif
-constexpr int kHostSlots = LNL_HOST_SLOTS;
+constexpr int kHostSlots = LNL_HOST_MAX_STREAMS;
+
+// One staging slot: its stream and device buffers, grown on demand.
+struct HostSlot {
+    hipStream_t stream = nullptr;
+    uint8_t* d_bytes = nullptr;
+    uint64_t* d_off = nullptr;
+    uint32_t* d_out = nullptr;
+    uint8_t* d_wire = nullptr;  // append: the chunk's wire burst
+    size_t cap_bytes = 0, cap_n = 0, cap_wire = 0;
+};
 
 struct DeviceState {
     std::once_flag once;
@@ -76,12 +84,7 @@ struct DeviceState {
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)
     std::mutex host_mu;
-    hipStream_t streams[kHostSlots] = {};
-    uint8_t* d_bytes[kHostSlots] = {};
-    uint64_t* d_off[kHostSlots] = {};
-    uint32_t* d_out[kHostSlots] = {};
-    uint8_t* d_wire[kHostSlots] = {};  // append: the chunk's wire burst
-    size_t cap_bytes = 0, cap_n = 0, cap_wire = 0;
+    HostSlot slot[kHostSlots];
 };
 
 DeviceState g_dev[kMaxDevices];
@@ -340,62 +343,120 @@ int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_
 #endif
 // The span path's scratch is kept per (device, stream) across calls: its two
 // control blocks (crc32c_span.h kSpanCtlWords) are used by alternate calls and
-// each call's batch kernel zeroes the other one's overflow count, and its
-// wave-batch boundary flags are reset by the span kernel itself, so no call
-// needs a memset or a pre-pass launch.  It grows stream-ordered (hipFreeAsync /
-// hipMallocAsync on the stream), and the blocks are zeroed once when it does.
-// g_span_mu is held from the parity's choice through the launches, so a
-// stream's calls take the blocks in launch order even from several threads.
+// each call's span kernel zeroes the other one's overflow count, and its
+// wave-batch boundary exchange blocks pair by the call's epoch (nothing is
+// reset), so no call needs a memset or a pre-pass launch.  It grows
+// stream-ordered (hipFreeAsync / hipMallocAsync on the stream), and the blocks
+// are zeroed once when it does.  The cache's mutex is held from the parity's
+// choice through the launches, so a stream's calls take the blocks and epochs
+// in launch order even from several threads.
+//
+// Keys.  A stream handle names one stream for every thread, except
+// hipStreamPerThread: each thread's launches on it go to that thread's own
+// stream, so its scratch is keyed by the thread as well (two threads sharing
+// one control block while their kernels run on different streams would race
+// on the exchange flags and the overflow count).  nullptr is the legacy null
+// stream in this library's launches (it is not built with per-thread default
+// streams), one stream for all threads.
+// Bound.  At most LNL_STREAM_CACHE streams' scratch is kept per device and map;
+// beyond that the least recently used entry is freed (after a device-wide
+// synchronize, since its stream may have been destroyed).  lnl_stream_release
+// frees a stream's entries explicitly, stream-ordered.
+struct StreamKey {
+    int dev;
+    hipStream_t st;
+    std::thread::id th;  // hipStreamPerThread only; default otherwise
+    bool operator<(const StreamKey& o) const {
+        if (dev != o.dev) return dev < o.dev;
+        if (st != o.st) return std::less<hipStream_t>()(st, o.st);
+        return th < o.th;
+    }
+};
+
+StreamKey stream_key(hipStream_t st) {
+    StreamKey k{0, st, std::thread::id()};
+    (void)hipGetDevice(&k.dev);
+    if (st == hipStreamPerThread) k.th = std::this_thread::get_id();
+    return k;
+}
+
 struct SpanScratch {
     uint32_t* buf = nullptr;
     size_t words = 0;
-    uint64_t calls = 0;
+    uint64_t calls = 0;  // span path: calls made on it (the control block parity and the exchange epoch)
+    uint64_t used = 0;   // LRU tick
 };
-std::mutex g_span_mu;
-std::map<std::pair<int, hipStream_t>, SpanScratch> g_span_scratch;
 
-int span_scratch(hipStream_t st, size_t words, size_t zero_words, uint32_t** buf, uint32_t* parity) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    SpanScratch& s = g_span_scratch[{dev, st}];
-    if (s.words < words) {
-        const size_t grow = words + words / 4;  // headroom: batches of similar sizes reuse it
-        if (s.buf) (void)hipFreeAsync(s.buf, st);
-        s.buf = nullptr;
-        s.words = 0;
-        hipError_t e = hipMallocAsync((void**)&s.buf, grow * sizeof(uint32_t), st);
-        if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", grow * 4, hipGetErrorString(e));
-        e = hipMemsetAsync(s.buf, 0, zero_words * sizeof(uint32_t), st);
-        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-        s.words = grow;
-        s.calls = 0;
+struct ScratchCache {
+    std::mutex mu;
+    std::map<StreamKey, SpanScratch> m;
+    uint64_t tick = 0;
+
+    // the entry for st, at least `words` long (the first zero_words zeroed
+    // whenever it is (re)allocated; *fresh says so); evicts beyond the bound
+    int get(hipStream_t st, size_t words, size_t zero_words, SpanScratch** out) {
+        const StreamKey key = stream_key(st);
+        SpanScratch& s = m[key];
+        s.used = ++tick;
+        if (s.words < words) {
+            const size_t grow = words + words / 4;  // headroom: batches of similar sizes reuse it
+            if (s.buf) (void)hipFreeAsync(s.buf, st);
+            s.buf = nullptr;
+            s.words = 0;
+            hipError_t e = hipMallocAsync((void**)&s.buf, grow * sizeof(uint32_t), st);
+            if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", grow * 4, hipGetErrorString(e));
+            if (zero_words && (e = hipMemsetAsync(s.buf, 0, zero_words * sizeof(uint32_t), st)) != hipSuccess)
+                return hip_fail(e, "hipMemsetAsync");
+            s.words = grow;
+            s.calls = 0;
+        }
+        *out = &s;
+        evict(key);
+        return 0;
     }
-    *buf = s.buf;
-    *parity = (uint32_t)(s.calls++ & 1u);
-    return 0;
+
+    void evict(const StreamKey& keep) {
+        size_t on_dev = 0;
+        for (auto& kv : m) on_dev += kv.first.dev == keep.dev;
+        if (on_dev <= (size_t)LNL_STREAM_CACHE) return;
+        auto victim = m.end();
+        for (auto it = m.begin(); it != m.end(); ++it) {
+            const bool same = !(it->first < keep) && !(keep < it->first);
+            if (it->first.dev == keep.dev && !same && (victim == m.end() || it->second.used < victim->second.used))
+                victim = it;
+        }
+        if (victim == m.end()) return;
+        // its stream may be gone: drain the device, then free on the null stream
+        (void)hipDeviceSynchronize();
+        if (victim->second.buf) (void)hipFreeAsync(victim->second.buf, nullptr);
+        m.erase(victim);
+    }
+
+    void release(hipStream_t st) {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = m.find(stream_key(st));
+        if (it == m.end()) return;
+        if (it->second.buf) (void)hipFreeAsync(it->second.buf, st);
+        m.erase(it);
+    }
+};
+
+ScratchCache g_span_cache;  // span path: mu held from the parity's choice through the launches
+
+int span_scratch(hipStream_t st, size_t words, size_t zero_words, SpanScratch** s) {
+    return g_span_cache.get(st, words, zero_words, s);
 }
 
 // The CSR XOR kernel's chunk map (lnl_xor.hip), kept per (device, stream) like
 // the span scratch: each call's map kernel rewrites the words its XOR kernel
 // reads, in stream order, so calls on one stream share it.
-std::mutex g_xor_mu;
-std::map<std::pair<int, hipStream_t>, SpanScratch> g_xor_scratch;
+ScratchCache g_xor_cache;
 
 int xor_map_scratch(hipStream_t st, size_t words, uint32_t** buf) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(g_xor_mu);
-    SpanScratch& s = g_xor_scratch[{dev, st}];
-    if (s.words < words) {
-        const size_t grow = words + words / 4;
-        if (s.buf) (void)hipFreeAsync(s.buf, st);
-        s.buf = nullptr;
-        s.words = 0;
-        hipError_t e = hipMallocAsync((void**)&s.buf, grow * sizeof(uint32_t), st);
-        if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", grow * 4, hipGetErrorString(e));
-        s.words = grow;
-    }
-    *buf = s.buf;
+    std::lock_guard<std::mutex> lk(g_xor_cache.mu);
+    SpanScratch* s = nullptr;
+    if (int rc = g_xor_cache.get(st, words, 0, &s)) return rc;
+    *buf = s->buf;
     return 0;
 }
 
@@ -419,21 +480,24 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
     g.waves = (uint32_t)S.cus * (uint32_t)(lnl::kSpanThreads / 64) * LNL_SPAN_ROUNDS;
     g.out = a.out;
     g.tab = S.span_tab;
-    std::lock_guard<std::mutex> lk(g_span_mu);
-    uint32_t* scratch = nullptr;
-    uint32_t parity = 0;
-    if (int rc = span_scratch(st, lnl::span_scratch_words(a.n, g.waves), lnl::span_scratch_zero_words(g.waves),
-                              &scratch, &parity))
+    std::lock_guard<std::mutex> lk(g_span_cache.mu);
+    SpanScratch* sc = nullptr;
+    if (int rc = span_scratch(st, lnl::span_scratch_words(a.n, g.waves), lnl::span_scratch_zero_words(g.waves), &sc))
         return rc;
-    lnl::span_scratch_layout(g, scratch, parity);
+    // control block: alternate calls; exchange epoch: one per call (>= 1: the
+    // zeroed arrival words hold epoch 0).  Both advance once the span kernel
+    // is launched -- it zeroes the next block's count itself, so a failed
+    // batch-kernel launch below leaves nothing stale for the next call.
+    lnl::span_scratch_layout(g, sc->buf, (uint32_t)(sc->calls & 1u));
+    g.epoch = sc->calls + 1u;
     if (span_ctl) *span_ctl = g.ctl;
     hipError_t e = lnl::launch_span(g, S.cus, st);
     if (e != hipSuccess) return hip_fail(e, "span kernel launch");
+    ++sc->calls;
     lnl::BatchArgs o = a;
     o.perm = g.ovf;
     o.perm_n = g.ctl + 1;
     o.span_ctl = g.ctl;
-    o.span_ctl_next = g.ctl_next;
     return launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st, LNL_SPAN_FIX_WGS);
 }
 
@@ -507,6 +571,29 @@ uint32_t run_plan(size_t stride, uint32_t len, uint32_t n, lnl::RunArgs& r) {
 }  // namespace
 
 extern "C" const char* lnl_crc32c_last_error(void) { return g_err.c_str(); }
+
+extern "C" int lnl_stream_release(void* hip_stream) {
+    g_span_cache.release((hipStream_t)hip_stream);
+    g_xor_cache.release((hipStream_t)hip_stream);
+    return 0;
+}
+
+extern "C" int lnl_diag_fill_span_arrivals(void* hip_stream, uint64_t value) {
+    const hipStream_t st = (hipStream_t)hip_stream;
+    DeviceState* S;
+    if (int rc = current_device(&S)) return rc;
+    std::lock_guard<std::mutex> lk(g_span_cache.mu);
+    auto it = g_span_cache.m.find(stream_key(st));
+    if (it == g_span_cache.m.end() || !it->second.buf) return fail(-ENOENT, "no span scratch kept for this stream");
+    const uint32_t waves = (uint32_t)S->cus * (uint32_t)(lnl::kSpanThreads / 64) * LNL_SPAN_ROUNDS;
+    const size_t blocks = lnl::span_max_segments(waves) / 64u;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    std::vector<uint64_t> v(blocks, value);
+    uint32_t* xch = it->second.buf + 2 * lnl::kSpanCtlWords + lnl::kSpanXchFlag;  // (span_scratch_layout)
+    e = hipMemcpy2D(xch, lnl::kSpanXchWords * 4u, v.data(), 8, 8, blocks, hipMemcpyHostToDevice);
+    return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpy2D");
+}
 
 extern "C" int lnl_crc32c_abi_version(void) { return LNL_CRC32C_ABI_VERSION; }
 
@@ -684,21 +771,76 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
 }
 }  // namespace
 
-// Host-resident batch: chunks of whole datagrams go round-robin over
-// kHostSlots streams; each chunk is H2D (bytes + offsets) -> kernel (offsets
-// rebased by off0) -> D2H (CRCs / statuses / the wire burst).  Stream order
-// makes buffer reuse safe; the streams overlap one chunk's copies with the
-// others' kernels and copies in the other direction.
+// Host-resident batch: chunks of whole datagrams go round-robin over the
+// call's streams (lnl_host_opts.streams); each chunk is H2D (bytes + offsets)
+// -> kernel (offsets rebased by off0) -> D2H (CRCs / statuses / the wire
+// burst).  Stream order makes buffer reuse safe; the streams overlap one
+// chunk's copies with the others' kernels and copies in the other direction.
 namespace {
 // Host-resident CSR batch through `device` (lnl_crc32c_batch_host,
-// lnl_inbound_filter_host, lnl_crc32c_append_host): chunks over kHostSlots
-// streams, H2D -> kernel -> D2H.
+// lnl_inbound_filter_host, lnl_crc32c_append_host and their _ex forms).
 enum HostMode : uint32_t { kHostCrc = 0, kHostFilter = 1, kHostAppend = 2 };
 // kHostCrc: h_out is u32 CRCs; kHostFilter: u8 inbound status codes;
 // kHostAppend: h_out is the wire burst (payload || LE32(CRC) per datagram,
 // back to back) and h_crc (optional) the CRCs
+
+// The resolved lnl_host_opts of one call.
+struct HostPlan {
+    int streams = LNL_HOST_DEFAULT_STREAMS;
+    uint32_t chunk_n = 1u << 16;
+    size_t chunk_bytes = size_t(64) << 20;
+};
+
+int host_plan(const lnl_host_opts* o, HostPlan* p) {
+    *p = HostPlan{};
+    if (!o) return 0;
+    if (o->size < sizeof(lnl_host_opts)) return fail(-EINVAL, "lnl_host_opts.size %u < %zu", o->size, sizeof(lnl_host_opts));
+    if (o->reserved) return fail(-EINVAL, "lnl_host_opts.reserved must be 0");
+    if (o->streams > (uint32_t)LNL_HOST_MAX_STREAMS)
+        return fail(-EINVAL, "lnl_host_opts.streams %u > %d", o->streams, LNL_HOST_MAX_STREAMS);
+    if (o->streams) p->streams = (int)o->streams;
+    if (o->chunk_datagrams) p->chunk_n = o->chunk_datagrams;
+    if (o->chunk_bytes) p->chunk_bytes = (size_t)o->chunk_bytes;
+    return 0;
+}
+
+// Slot k holds at least these sizes (its stream created on first use; buffers
+// regrown only when a call needs more).  Freeing a slot's buffers is safe
+// here: the previous call on this device drained every slot's stream.
+int slot_ready(HostSlot& s, size_t need_bytes, size_t need_n, size_t need_wire) {
+    hipError_t e;
+    if (!s.stream && (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(e, "hipStreamCreate");
+    if (need_bytes > s.cap_bytes || need_n > s.cap_n) {
+        (void)hipFree(s.d_bytes);
+        (void)hipFree(s.d_off);
+        (void)hipFree(s.d_out);
+        s.d_bytes = nullptr;
+        s.d_off = nullptr;
+        s.d_out = nullptr;
+        s.cap_bytes = s.cap_n = 0;
+        const size_t nb = std::max<size_t>(need_bytes, 256);
+        if ((e = hipMalloc(&s.d_bytes, nb)) != hipSuccess || (e = hipMalloc(&s.d_off, (need_n + 1) * 8)) != hipSuccess ||
+            (e = hipMalloc(&s.d_out, need_n * 4)) != hipSuccess)
+            return fail(-ENOMEM, "staging allocation: %s", hipGetErrorString(e));
+        s.cap_bytes = nb;
+        s.cap_n = need_n;
+    }
+    if (need_wire > s.cap_wire) {  // the wire staging: append calls only
+        (void)hipFree(s.d_wire);
+        s.d_wire = nullptr;
+        s.cap_wire = 0;
+        if ((e = hipMalloc(&s.d_wire, need_wire)) != hipSuccess)
+            return fail(-ENOMEM, "wire staging allocation: %s", hipGetErrorString(e));
+        s.cap_wire = need_wire;
+    }
+    return 0;
+}
+
 int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h_out, int device,
-               uint32_t mode, uint32_t* h_crc = nullptr) {
+               uint32_t mode, uint32_t* h_crc, const lnl_host_opts* opts) {
+    HostPlan plan;
+    if (int rc = host_plan(opts, &plan)) return rc;
     if (n == 0) return 0;
     if (!h_base || !h_off || !h_out) return fail(-EINVAL, "NULL argument");
     const uint32_t filter = mode == kHostFilter;
@@ -716,135 +858,111 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         ~Restore() { (void)hipSetDevice(d); }
     } restore{prev};
 
-    constexpr size_t kChunkBytes = size_t(64) << 20;  // per stream
-    constexpr uint32_t kChunkN = 1u << 16;
-    // chunk boundaries: <= kChunkN datagrams and <= kChunkBytes bytes (a single
+    const int ns = plan.streams;
+    // chunk boundaries: <= chunk_n datagrams and <= chunk_bytes bytes (a single
     // larger datagram gets a chunk of its own)
+    auto chunk_end = [&](uint32_t i) {
+        uint32_t j = i + 1;
+        while (j < n && j - i < plan.chunk_n && h_off[j + 1] - h_off[i] <= plan.chunk_bytes) ++j;
+        return j;
+    };
     size_t need_bytes = 0;
     uint32_t need_n = 0;
-    {
-        uint32_t i = 0;
-        while (i < n) {
-            uint32_t j = i + 1;
-            while (j < n && j - i < kChunkN && h_off[j + 1] - h_off[i] <= kChunkBytes) ++j;
-            need_bytes = std::max<size_t>(need_bytes, h_off[j] - h_off[i]);
-            need_n = std::max(need_n, j - i);
-            i = j;
-        }
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t j = chunk_end(i);
+        need_bytes = std::max<size_t>(need_bytes, h_off[j] - h_off[i]);
+        need_n = std::max(need_n, j - i);
+        i = j;
     }
-    if (!S->streams[0]) {
-        for (int k = 0; k < kHostSlots; ++k)
-            if ((e = hipStreamCreateWithFlags(&S->streams[k], hipStreamNonBlocking)) != hipSuccess)
-                return hip_fail(e, "hipStreamCreate");
-    }
-    if (need_bytes > S->cap_bytes || need_n > S->cap_n) {
-        for (int k = 0; k < kHostSlots; ++k) {
-            (void)hipFree(S->d_bytes[k]);
-            (void)hipFree(S->d_off[k]);
-            (void)hipFree(S->d_out[k]);
-            (void)hipFree(S->d_wire[k]);
-            S->d_bytes[k] = nullptr;
-            S->d_off[k] = nullptr;
-            S->d_out[k] = nullptr;
-            S->d_wire[k] = nullptr;
-        }
-        S->cap_bytes = S->cap_n = S->cap_wire = 0;
-        const size_t nb = std::max<size_t>(need_bytes, 256);
-        for (int k = 0; k < kHostSlots; ++k) {
-            if ((e = hipMalloc(&S->d_bytes[k], nb)) != hipSuccess ||
-                (e = hipMalloc(&S->d_off[k], (size_t)(need_n + 1) * 8)) != hipSuccess ||
-                (e = hipMalloc(&S->d_out[k], (size_t)need_n * 4)) != hipSuccess)
-                return fail(-ENOMEM, "staging allocation: %s", hipGetErrorString(e));
-        }
-        S->cap_bytes = nb;
-        S->cap_n = need_n;
-    }
-    const size_t need_wire = S->cap_bytes + (size_t)S->cap_n * LNL_CRC32C_LAYER_EXTRA;
-    if (mode == kHostAppend && need_wire > S->cap_wire) {  // the wire staging, on the first append only
-        for (int k = 0; k < kHostSlots; ++k) {
-            (void)hipFree(S->d_wire[k]);
-            S->d_wire[k] = nullptr;
-        }
-        S->cap_wire = 0;
-        for (int k = 0; k < kHostSlots; ++k)
-            if ((e = hipMalloc(&S->d_wire[k], need_wire)) != hipSuccess)
-                return fail(-ENOMEM, "wire staging allocation: %s", hipGetErrorString(e));
-        S->cap_wire = need_wire;
-    }
-    // after the first enqueue, every error path drains both streams first: the
+    const size_t need_wire = mode == kHostAppend ? need_bytes + (size_t)need_n * LNL_CRC32C_LAYER_EXTRA : 0;
+    for (int k = 0; k < ns; ++k)
+        if (int rc = slot_ready(S->slot[k], need_bytes, need_n, need_wire)) return rc;
+    // after the first enqueue, every error path drains the streams first: the
     // caller may free h_base / h_out as soon as we return
     auto drained = [&](int rc) {
-        for (int s2 = 0; s2 < kHostSlots; ++s2) (void)hipStreamSynchronize(S->streams[s2]);
+        for (int s2 = 0; s2 < ns; ++s2) (void)hipStreamSynchronize(S->slot[s2].stream);
         return rc;
     };
     uint32_t i = 0;
     int k = 0;
     while (i < n) {
-        uint32_t j = i + 1;
-        while (j < n && j - i < kChunkN && h_off[j + 1] - h_off[i] <= kChunkBytes) ++j;
+        const uint32_t j = chunk_end(i);
         const uint32_t cn = j - i;
         const size_t cb = h_off[j] - h_off[i];
-        hipStream_t st = S->streams[k];
-        if (cb && (e = hipMemcpyAsync(S->d_bytes[k], h_base + h_off[i], cb, hipMemcpyHostToDevice, st)) !=
-                      hipSuccess)
+        HostSlot& s = S->slot[k];
+        hipStream_t st = s.stream;
+        if (cb && (e = hipMemcpyAsync(s.d_bytes, h_base + h_off[i], cb, hipMemcpyHostToDevice, st)) != hipSuccess)
             return drained(hip_fail(e, "H2D bytes"));
-        if ((e = hipMemcpyAsync(S->d_off[k], h_off + i, (size_t)(cn + 1) * 8, hipMemcpyHostToDevice, st)) !=
-            hipSuccess)
+        if ((e = hipMemcpyAsync(s.d_off, h_off + i, (size_t)(cn + 1) * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
             return drained(hip_fail(e, "H2D offsets"));
         lnl::BatchArgs a{};
-        a.base = S->d_bytes[k];
-        a.off = S->d_off[k];
+        a.base = s.d_bytes;
+        a.off = s.d_off;
         a.off0 = h_off[i];
         a.n = cn;
         const size_t esz = filter ? 1 : 4;  // bytes of output per datagram
         if (mode == kHostAppend) {
             // the chunk's wire burst starts where its first datagram's wire
             // bytes go: (h_off[i] - h_off[0]) + 4 i
-            if (int rc = append_csr(*S, a, S->d_wire[k], S->d_out[k], st)) return drained(rc);
+            if (int rc = append_csr(*S, a, s.d_wire, s.d_out, st)) return drained(rc);
             uint8_t* dst = (uint8_t*)h_out + (h_off[i] - h_off[0]) + (size_t)i * LNL_CRC32C_LAYER_EXTRA;
-            if ((e = hipMemcpyAsync(dst, S->d_wire[k], cb + (size_t)cn * LNL_CRC32C_LAYER_EXTRA,
-                                    hipMemcpyDeviceToHost, st)) != hipSuccess)
+            if ((e = hipMemcpyAsync(dst, s.d_wire, cb + (size_t)cn * LNL_CRC32C_LAYER_EXTRA, hipMemcpyDeviceToHost,
+                                    st)) != hipSuccess)
                 return drained(hip_fail(e, "D2H wire"));
-            if (h_crc && (e = hipMemcpyAsync(h_crc + i, S->d_out[k], (size_t)cn * 4, hipMemcpyDeviceToHost, st)) !=
+            if (h_crc && (e = hipMemcpyAsync(h_crc + i, s.d_out, (size_t)cn * 4, hipMemcpyDeviceToHost, st)) !=
                              hipSuccess)
                 return drained(hip_fail(e, "D2H crc"));
-            i = j;
-            k = (k + 1) % kHostSlots;
-            continue;
-        }
-        if (filter) {
-            a.ok = (uint8_t*)S->d_out[k];
-            a.filter = 1;
-            if (int rc = launch_csr(*S, a, lnl::kModeVerify, st)) return drained(rc);
         } else {
-            a.out = S->d_out[k];
-            if (int rc = launch_csr(*S, a, lnl::kModeCsr, st)) return drained(rc);
+            if (filter) {
+                a.ok = (uint8_t*)s.d_out;
+                a.filter = 1;
+                if (int rc = launch_csr(*S, a, lnl::kModeVerify, st)) return drained(rc);
+            } else {
+                a.out = s.d_out;
+                if (int rc = launch_csr(*S, a, lnl::kModeCsr, st)) return drained(rc);
+            }
+            if ((e = hipMemcpyAsync((uint8_t*)h_out + (size_t)i * esz, s.d_out, (size_t)cn * esz,
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return drained(hip_fail(e, "D2H"));
         }
-        if ((e = hipMemcpyAsync((uint8_t*)h_out + (size_t)i * esz, S->d_out[k], (size_t)cn * esz,
-                                hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return drained(hip_fail(e, "D2H"));
         i = j;
-        k = (k + 1) % kHostSlots;
+        k = (k + 1) % ns;
     }
-    for (int s = 0; s < kHostSlots; ++s)
-        if ((e = hipStreamSynchronize(S->streams[s])) != hipSuccess) return drained(hip_fail(e, "hipStreamSynchronize"));
+    for (int s = 0; s < ns; ++s)
+        if ((e = hipStreamSynchronize(S->slot[s].stream)) != hipSuccess)
+            return drained(hip_fail(e, "hipStreamSynchronize"));
     return 0;
 }
 }  // namespace
 
 extern "C" int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                                      uint32_t* h_out, int device) {
-    return host_batch(h_base, h_off, n, h_out, device, kHostCrc);
+    return host_batch(h_base, h_off, n, h_out, device, kHostCrc, nullptr, nullptr);
 }
 
 extern "C" int lnl_inbound_filter_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                                        uint8_t* h_status, int device) {
-    return host_batch(h_base, h_off, n, h_status, device, kHostFilter);
+    return host_batch(h_base, h_off, n, h_status, device, kHostFilter, nullptr, nullptr);
 }
 
 extern "C" int lnl_crc32c_append_host(const uint8_t* h_payload, const uint64_t* h_off, uint32_t n, uint8_t* h_wire,
                                       uint32_t* h_crc, int device) {
-    return host_batch(h_payload, h_off, n, h_wire, device, kHostAppend, h_crc);
+    return host_batch(h_payload, h_off, n, h_wire, device, kHostAppend, h_crc, nullptr);
+}
+
+extern "C" int lnl_crc32c_batch_host_ex(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, uint32_t* h_out,
+                                        int device, const lnl_host_opts* opts) {
+    return host_batch(h_base, h_off, n, h_out, device, kHostCrc, nullptr, opts);
+}
+
+extern "C" int lnl_inbound_filter_host_ex(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
+                                          uint8_t* h_status, int device, const lnl_host_opts* opts) {
+    return host_batch(h_base, h_off, n, h_status, device, kHostFilter, nullptr, opts);
+}
+
+extern "C" int lnl_crc32c_append_host_ex(const uint8_t* h_payload, const uint64_t* h_off, uint32_t n,
+                                         uint8_t* h_wire, uint32_t* h_crc, int device, const lnl_host_opts* opts) {
+    return host_batch(h_payload, h_off, n, h_wire, device, kHostAppend, h_crc, opts);
 }
 
 extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,

@@ -35,11 +35,10 @@ struct BatchArgs {
     const uint32_t* perm_n;  // optional (device): number of perm entries, else n
     const uint32_t* tail_xor;  // optional: out[i] ^= tail_xor[i] for all i < n first (CSR uniform path)
     uint32_t xor_n;            // entries of tail_xor
-    // optional (CSR span path): the span kernel's control block ([2] == 0:
-    // it did not take the batch, so this kernel takes all of it) and the next
-    // call's, whose overflow count this kernel zeroes (crc32c_span.h)
+    // optional (CSR span path): the span kernel's control block ([1] the
+    // overflow count, the list in perm; [2] == 0: it did not take the batch,
+    // so this kernel takes all of it; crc32c_span.h)
     const uint32_t* span_ctl;
-    uint32_t* span_ctl_next;
 };
 
 // Enqueue one batch kernel on `stream` with `grid` workgroups.
@@ -180,8 +179,9 @@ struct SpanArgs {
     const uint32_t* tab;     // kSpanTabWords words (lnl_build_span_tables)
     uint32_t* ctl;           // this call's control block: [1] overflow datagrams (0 on entry),
                              // [2] segments (0: the batch kernel takes the whole batch), [3] R
-    uint32_t* ctl_next;      // the other block: the next call's, zeroed by this call's batch kernel
+    uint32_t* ctl_next;      // the other block: the next call's, its count zeroed by this call's span kernel
     uint32_t* xch;           // per wave-batch boundary: exchange block (crc32c_span.h kSpanXch*)
+    uint64_t epoch;          // this call's exchange epoch (>= 1, one per call on the scratch)
     uint32_t* ovf;           // n: datagrams left to the batch kernel
     // verify modes (kSpanVerify, kSpanFilter): ok[i] instead of out[i]
     uint32_t mode;

@@ -271,18 +271,23 @@ __global__ __launch_bounds__(kBlockThreads, 2) void crc32c_batch_kernel(BatchArg
             if (v) a.out[i] ^= v;
         }
     }
-    // CSR span path (the span kernel combined the cross-segment heads itself):
-    // zero the next call's overflow count; take the whole batch when the span
-    // kernel did not
+    // CSR span path (the span kernel combined the cross-segment heads itself
+    // and zeroed the next call's overflow count): the overflow list, or the
+    // whole batch when the span kernel did not take it -- [1] and [2] of its
+    // control block in one load
+    uint32_t nperm;
     if (a.span_ctl) {
-        if (blockIdx.x == 0 && threadIdx.x == 0 && a.span_ctl_next) a.span_ctl_next[1] = 0u;
-        if (a.span_ctl[2] == 0u) {
+        const uint4 c = *reinterpret_cast<const uint4*>(a.span_ctl);  // (32-byte aligned control blocks)
+        const bool taken = uni(c.z) != 0u;
+        nperm = taken ? uni(c.y) : a.n;
+        if (!taken) {
             a.perm = nullptr;
             a.perm_n = nullptr;
         }
+    } else {
+        // entries to process: n, or a device-side count of perm entries
+        nperm = a.perm_n ? uni(*a.perm_n) : a.n;
     }
-    // entries to process: n, or a device-side count of perm entries
-    const uint32_t nperm = a.perm_n ? uni(*a.perm_n) : a.n;
     const uint32_t nbatch = (nperm + 63u) >> 6;
     if (blockIdx.x * kWaves >= nbatch) return;  // whole workgroup idle (before the barrier)
 

@@ -74,13 +74,21 @@ LNL_HD LNL_INLINE bool span_overflow(uint64_t Pi, uint64_t Pj, uint32_t R) {
 // boundary in the stream's scratch (kSpanXch*).
 // hinfo word: m | e << 8 | head tracked << 16
 constexpr uint32_t kSpanHeadBit = 1u << 16;
-// exchange block of wave-batch boundary w (words): the flag (arrivals: 0
-// between calls), the tail side (lane 63 of w - 1: its register value, its
+// exchange block of wave-batch boundary w (words): the arrival word (u64,
+// words 0-1), the tail side (lane 63 of w - 1: its register value, its
 // datagram's start in the segment | header byte << 16) and the head side (lane
-// 0 of w: register value, datagram index, hinfo)
-constexpr uint32_t kSpanXchFlag = 0, kSpanXchTail = 1, kSpanXchTailInfo = 2, kSpanXchHead = 3,
-                   kSpanXchHeadIdx = 4, kSpanXchHeadInfo = 5;
+// 0 of w: register value, datagram index, hinfo).
+// Arrival: each side stores its part, drains it (vmcnt(0)), then swaps
+// span_arrival(epoch, side) into the arrival word.  The side whose swap
+// returns span_arrival(epoch, other side) arrived second and combines.  The
+// epoch is the call's (SpanArgs::epoch, one per call on a scratch buffer), so
+// whatever an earlier call -- finished or aborted -- left in the word never
+// pairs: no word has to be reset between calls.
+constexpr uint32_t kSpanXchFlag = 0, kSpanXchTail = 2, kSpanXchTailInfo = 3, kSpanXchHead = 4,
+                   kSpanXchHeadIdx = 5, kSpanXchHeadInfo = 6;
 constexpr uint32_t kSpanXchWords = 8;  // one 32-byte sector per boundary
+constexpr uint32_t kSpanSideHead = 1, kSpanSideTail = 2;
+LNL_HD LNL_INLINE uint64_t span_arrival(uint64_t epoch, uint32_t side) { return (epoch << 2) | side; }
 
 // ---- verify modes ---------------------------------------------------------------
 // The span kernel checks a wire datagram (payload || LE32(CRC)) without

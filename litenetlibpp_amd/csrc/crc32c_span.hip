@@ -341,6 +341,9 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the batch kernel and the dispatch fix-up
         A.ctl[2] = runs ? G.NS : 0u;             // 0: the whole batch is the batch kernel's
         A.ctl[3] = G.R;
+        // the next call's overflow count (the previous call on this stream,
+        // which used that block, has finished: stream order)
+        A.ctl_next[1] = 0u;
     }
     if (!runs) return;
     const uint32_t R = G.R, Sb = R << 7, NS = G.NS, nwb = G.nwb;
@@ -1073,12 +1076,15 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // Wave-batch boundaries: lane 0's head came in from wave-batch wb - 1's
         // lane 63, lane 63's tail goes on to wb + 1's lane 0.  Each side writes
         // its part into the boundary's exchange block (crc32c_span.h kSpanXch*)
-        // and then arrives at its flag; the side that arrives second has both
-        // parts and combines them, then resets the flag for the stream's next
-        // call.  The parts are device-scope (sc1) stores and loads and the flag
-        // a device-scope atomic, ordered by a vmcnt(0) between the stores and
-        // the arrival: no L2 writeback or invalidate (an acq_rel fence at agent
-        // scope does both on gfx950, per wave, and measured 35 us slower).
+        // and then swaps its arrival (the call's epoch and its side) into the
+        // block's arrival word; the side whose swap returns the other side's
+        // arrival of this epoch has both parts and combines them.  Nothing is
+        // reset: a word left by an earlier call (or by an aborted one) holds
+        // another epoch and never pairs.  The parts are device-scope (sc1)
+        // stores and loads and the arrival a device-scope atomic, ordered by a
+        // vmcnt(0) between the stores and the arrival: no L2 writeback or
+        // invalidate (an acq_rel fence at agent scope does both on gfx950, per
+        // wave, and measured 35 us slower).
         if (live && (lane == 0u || lane == 63u)) {
             const uint32_t w = lane == 0u ? wb : wb + 1u;  // boundary w: segments 64 w - 1 | 64 w
             if (w != 0u && w < nwb) {
@@ -1089,6 +1095,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 auto get_x = [&](uint32_t i) -> uint32_t {
                     return __hip_atomic_load(xb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 };
+                const uint32_t side = lane == 0u ? kSpanSideHead : kSpanSideTail;
                 if (lane == 0u) {
                     put_x(kSpanXchHead, r_head);
                     put_x(kSpanXchHeadIdx, hk);
@@ -1098,7 +1105,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     put_x(kSpanXchTailInfo, tcs | (thdr << 16));
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the parts are out before the arrival
-                if (__hip_atomic_fetch_add(xb + kSpanXchFlag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+                const uint64_t prior = __hip_atomic_exchange(reinterpret_cast<uint64_t*>(xb + kSpanXchFlag),
+                                                             span_arrival(A.epoch, side), __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+                if (prior == span_arrival(A.epoch, kSpanSideHead ^ kSpanSideTail ^ side)) {
                     const uint32_t head = lane == 0u ? r_head : get_x(kSpanXchHead);
                     const uint32_t hidx = lane == 0u ? hk : get_x(kSpanXchHeadIdx);
                     const uint32_t info = lane == 0u ? (hinfo | (htrack ? kSpanHeadBit : 0u)) : get_x(kSpanXchHeadInfo);
@@ -1109,7 +1119,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                         const uint32_t crc = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tail) ^ head);
                         store_result(A, hidx, crc, (Sb - (tinf & 0xFFFFu)) + (m << 7) - e, tinf >> 16);
                     }
-                    __hip_atomic_store(xb + kSpanXchFlag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
@@ -1128,9 +1137,9 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 }  // namespace
 
 // Scratch: two 8-word control blocks (crc32c_span.h kSpanCtl*) and the
-// wave-batch boundaries' exchange blocks (kSpanXch*: their flags are zero
-// between calls, so all of it is zeroed once at allocation), then the overflow
-// list.
+// wave-batch boundaries' exchange blocks (kSpanXch*: arrival words of epoch 0
+// until a call writes them; all of it zeroed once at allocation), then the
+// overflow list.
 size_t span_scratch_zero_words(uint32_t waves) {
     return 2 * kSpanCtlWords + (size_t)(span_max_segments(waves) / 64u) * kSpanXchWords;
 }

@@ -13,10 +13,13 @@
 // kernel refuses gets its negative errno in status[i] (send_raw returns -1 for
 // host / network unreachable and raises a NETWORK_ERROR event, 0 for other
 // errors: the caller maps status to that) and the burst goes on with the next
-// one.  A full socket buffer (EAGAIN) is not a per-datagram error: with
-// wait_ms != 0 the call polls for POLLOUT (-1: forever) and continues, with 0
-// (or when the wait expires) it returns early and the datagrams from the
-// returned count on were not attempted.
+// one; that includes ENOBUFS (the interface queue, not the socket buffer, is
+// full: poll would report POLLOUT at once and the call would spin).  A full
+// socket buffer (EAGAIN) is not a per-datagram error: with wait_ms != 0 the
+// call polls for POLLOUT and continues, until one deadline of wait_ms from the
+// call's start (-1: no deadline); with 0, or once the deadline has passed, it
+// returns early and the datagrams from the returned count on were not
+// attempted.
 //
 // CPU only (no HIP): it is the socket side of the path.
 #include <errno.h>
@@ -25,6 +28,7 @@
 #include <string.h>
 #include <sys/socket.h>
 
+#include <chrono>
 #include <vector>
 
 #include "../../include/lnl_crc32c.h"
@@ -46,6 +50,8 @@ extern "C" int64_t lnl_egress_send_batch(int fd, const uint8_t* wire, const uint
         msgs.resize(kMaxVec);
         iov.resize(kMaxVec);
     }
+    using clock = std::chrono::steady_clock;
+    const clock::time_point deadline = clock::now() + std::chrono::milliseconds(wait_ms > 0 ? wait_ms : 0);
     uint32_t i = 0;
     while (i < n) {
         const uint32_t k = n - i < kMaxVec ? n - i : kMaxVec;
@@ -72,16 +78,22 @@ extern "C" int64_t lnl_egress_send_batch(int fd, const uint8_t* wire, const uint
         // error only when nothing was sent)
         const int err = r < 0 ? errno : EAGAIN;
         if (err == EINTR) continue;
-        if (err == EAGAIN || err == EWOULDBLOCK || err == ENOBUFS) {
+        if (err == EAGAIN || err == EWOULDBLOCK) {
             if (wait_ms == 0) return (int64_t)i;
+            int left = -1;  // wait_ms < 0: no deadline
+            if (wait_ms > 0) {
+                const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - clock::now()).count();
+                if (ms <= 0) return (int64_t)i;  // deadline passed: datagrams i.. not attempted
+                left = (int)ms;
+            }
             pollfd p{fd, POLLOUT, 0};
-            const int pr = poll(&p, 1, wait_ms);
+            const int pr = poll(&p, 1, left);
             if (pr < 0 && errno != EINTR) return -errno;
             if (pr == 0) return (int64_t)i;  // wait expired: datagrams i.. not attempted
             continue;
         }
         if (err == EBADF || err == ENOTSOCK) return -err;  // the call itself is wrong, not a datagram
-        // a per-datagram failure (EHOSTUNREACH, ENETUNREACH, EMSGSIZE,
+        // a per-datagram failure (EHOSTUNREACH, ENETUNREACH, EMSGSIZE, ENOBUFS,
         // ECONNREFUSED from an earlier ICMP, ...): send_raw's error case for
         // this datagram, then the next one
         if (status) status[i] = -(int64_t)err;

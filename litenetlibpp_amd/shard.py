@@ -3,7 +3,9 @@ ranges, no collective on the data path.
 
 The only collectives used by the benchmark are a barrier and a MAX over the
 per-rank times (timing, not data).  Works with any torch.distributed backend
-("nccl" = RCCL on the GPU box, "gloo" in the CPU tests).
+("nccl" = RCCL on the GPU box, "gloo" in the CPU tests).  The reductions run
+whenever a process group is initialised -- also at world size 1, which is how
+``bench.py --force-dist`` exercises the RCCL branch on one GPU.
 """
 from __future__ import annotations
 
@@ -22,7 +24,7 @@ def max_over_ranks(value: float, device=None) -> float:
     """MAX of a per-rank scalar (the job's time is its slowest rank's)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -33,7 +35,7 @@ def gather_over_ranks(value: float, device=None) -> list[float]:
     """Every rank's scalar, in rank order (reporting only)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [float(value)]
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
@@ -44,7 +46,7 @@ def gather_over_ranks(value: float, device=None) -> list[float]:
 def sum_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t)

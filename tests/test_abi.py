@@ -38,7 +38,9 @@ def test_header_declares_the_boundary():
               "lnl_crc32c_batch_host_multi", "lnl_packet_verify", "lnl_inbound_status",
               "lnl_inbound_filter_csr_dev", "lnl_inbound_filter_host", "lnl_ingress_recv_batch",
               "lnl_dispatch_csr_dev", "lnl_inbound_filter_dispatch_csr_dev", "lnl_xor_layer", "lnl_xor_layer_csr_dev", "lnl_xor_layer_fixed_dev",
-              "lnl_crc32c_append_host", "lnl_egress_send_batch"):
+              "lnl_crc32c_append_host", "lnl_egress_send_batch", "lnl_crc32c_batch_host_ex",
+              "lnl_inbound_filter_host_ex", "lnl_crc32c_append_host_ex", "lnl_stream_release",
+              "lnl_diag_fill_span_arrivals"):
         assert s in syms
 
 
@@ -48,7 +50,7 @@ def test_library_exports_every_declared_symbol(pkg):
     exported = set(re.findall(r"\bT (lnl_\w+)", out))
     missing = [s for s in declared_symbols() if s not in exported]
     assert not missing, missing
-    assert pkg.lib().lnl_crc32c_abi_version() == 8
+    assert pkg.lib().lnl_crc32c_abi_version() == 9
 
 
 def test_ctypes_bindings_match_the_header(pkg):
@@ -173,3 +175,37 @@ def test_host_batch_offsets_checked_before_the_call(pkg):
                    lambda o: pkg.egress_send_batch(0, data, o)):
             with pytest.raises(ValueError):
                 fn(off)
+
+
+def test_host_opts_checked_without_gpu(pkg):
+    """lnl_host_opts (include/lnl_crc32c.h) is validated before anything else:
+    a bad size, a nonzero reserved field or more than LNL_HOST_MAX_STREAMS
+    streams give -EINVAL even for an empty batch; good options on a machine
+    without a GPU give -ENODEV, never a CPU answer."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present; covered by the gpu suite")
+    L = pkg.lib()
+    assert ctypes.sizeof(pkg.HostOpts) == 24
+    buf = (ctypes.c_uint8 * 64)()
+    off = (ctypes.c_uint64 * 3)(0, 16, 64)
+    out = (ctypes.c_uint32 * 2)()
+    bad = [pkg.HostOpts.make(streams=9), pkg.HostOpts(8, 2, 0, 0, 0), pkg.HostOpts(24, 2, 0, 1, 0)]
+    for o in bad:
+        for n in (0, 2):
+            assert L.lnl_crc32c_batch_host_ex(ctypes.addressof(buf), ctypes.addressof(off), n, ctypes.addressof(out),
+                                              0, ctypes.pointer(o)) == -22
+            assert L.lnl_inbound_filter_host_ex(ctypes.addressof(buf), ctypes.addressof(off), n,
+                                                ctypes.addressof(out), 0, ctypes.pointer(o)) == -22
+            assert L.lnl_crc32c_append_host_ex(ctypes.addressof(buf), ctypes.addressof(off), n,
+                                               ctypes.addressof(buf), None, 0, ctypes.pointer(o)) == -22
+    good = pkg.HostOpts.make(streams=2, chunk_datagrams=1)
+    assert L.lnl_crc32c_batch_host_ex(ctypes.addressof(buf), ctypes.addressof(off), 0, ctypes.addressof(out), 0,
+                                      ctypes.pointer(good)) == 0
+    assert L.lnl_crc32c_batch_host_ex(ctypes.addressof(buf), ctypes.addressof(off), 2, ctypes.addressof(out), 0,
+                                      ctypes.pointer(good)) == -19
+    assert L.lnl_crc32c_batch_host_ex(ctypes.addressof(buf), ctypes.addressof(off), 2, ctypes.addressof(out), 0,
+                                      None) == -19
+    assert list(out) == [0, 0]
+    with pytest.raises(ValueError):
+        pkg.batch_host(np.zeros(64, np.uint8), np.array([0, 64], np.uint64), 0, streams=9)

@@ -74,3 +74,17 @@ def test_every_workload_names_its_metric():
         assert line["n_gpus"] == 1 and line["unit"] == "GB/s" and line["higher_is_better"]
         seen.add((line["metric"], line["config"]["workload"]))
     assert len(seen) == 9
+
+
+def test_force_dist_at_one_rank():
+    """--force-dist at --gpus 1 initialises the process group and runs every
+    collective of the N-rank path (here gloo, dry run; RCCL on the GPU box:
+    tests/test_gpu_config4.py), then tears it down."""
+    r = _run(["--gpus", "1", "--force-dist", "--steps", "2", "--warmup", "0", "--packets", "64"])
+    assert r.returncode == 0, r.stderr
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert line["n_gpus"] == 1
+    assert line["distributed"]["forced"] is True and line["distributed"]["world_size"] == 1
+    r = _run(["--gpus", "1", "--steps", "2", "--warmup", "0", "--packets", "64"])
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert line["distributed"] is None

@@ -510,7 +510,7 @@ def test_socket_path_end_to_end(P):
 @pytest.mark.parametrize("n,shift", [(1, 0), (777, 3), (200_000, 11)])
 def test_append_host_matches_layer_outbound(P, n, shift):
     """lnl_crc32c_append_host (pinned payload burst -> H2D -> CRC + append ->
-    D2H, chunks over 2 streams; 200,000 datagrams take several chunks): every
+    D2H, chunks over the default 4 streams; 200,000 datagrams take several chunks): every
     wire byte equals lnl_crc32c_layer_outbound of its payload, back to back, and
     the CRCs equal the oracle's.  Nonzero first offset."""
     rng = np.random.default_rng(400 + n)
