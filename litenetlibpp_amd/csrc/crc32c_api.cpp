@@ -183,23 +183,16 @@ int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st, uin
 #ifndef LNL_BUCKET_MIN_N
 #define LNL_BUCKET_MIN_N 16384
 #endif
-// CSR kernel selection.  The product library has one path: the bucketed batch
-// kernel.  The experiments build (-DLNL_EXPERIMENTS=1, tools/kvariants.py,
-// build/variants/*.so -- never loaded by the product path) adds three more,
-// selected with lnl_crc32c_set_csr_path() or LNL_CSR_PATH:
-//   uniform  crc32c_csr.hip: uniform line-count batches, shared lines fetched
-//            once (786 MB instead of 968 MB per config-3 batch) -- but its
-//            kernel streams them slower and its plan + tail epilogue cost more:
-//            0.188 vs 0.175 ms per config-3 batch
-//   seg      crc32c_seg.hip: VALU-bound (datagram ends fall on different rows
-//            in each lane, so nearly every row pays a divergent fold): 0.33 ms
-//   pairs    crc32c_pair.hip: 13 % fewer bytes, streamed at ~5.0 TB/s: 0.233 ms
-// The initial value comes from the environment (LNL_CSR_PATH=bucketed |
-// uniform | seg | pairs).
-// kPathBucketed (0) is the product: the span kernel for CSR batches, the
-// bucketed batch kernel for verify / filter batches; kPathBucketCsr (4) runs
-// CSR batches through the bucketed batch kernel too (the previous default)
-enum CsrPath : int { kPathBucketed = 0, kPathUniform = 1, kPathSeg = 2, kPathPairs = 3, kPathBucketCsr = 4 };
+// CSR kernel selection.  The product library has one path per mode: the span
+// kernel for large CSR and status-only verify / filter batches, the bucketed
+// batch kernel for verify batches that also want body CRCs.  The experiments
+// build (-DLNL_EXPERIMENTS=1, tools/kvariants.py, build/variants/*.so -- never
+// loaded by the product path) can send large CSR batches through the bucketed
+// batch kernel instead (lnl_crc32c_set_csr_path(4) or LNL_CSR_PATH=bucketed).
+// The round-1 experiment kernels (uniform, segment and pair paths, and the
+// verify-from-wire epilogue) are kept as tools/experiments/csr_experiment_kernels.patch
+// (DESIGN 4.6).
+enum CsrPath : int { kPathBucketed = 0, kPathBucketCsr = 4 };
 #if !LNL_EXPERIMENTS
 constexpr int csr_path() { return kPathBucketed; }
 #else
@@ -209,130 +202,13 @@ int csr_path() {
     if (p >= 0) return p;
     p = kPathBucketed;
     if (const char* e = getenv("LNL_CSR_PATH")) {
-        if (!strcmp(e, "uniform")) p = kPathUniform;
-        else if (!strcmp(e, "seg")) p = kPathSeg;
-        else if (!strcmp(e, "pairs")) p = kPathPairs;
-        else if (!strcmp(e, "bucketed")) p = kPathBucketCsr;
+        if (!strcmp(e, "bucketed")) p = kPathBucketCsr;
     }
     int expect = -1;
     g_csr_path.compare_exchange_strong(expect, p);
     return g_csr_path.load();
 }
 
-// CSR batches: the pair kernel (crc32c_pair.hip) after its bucket pre-pass;
-// pairs with very long datagrams go to the batch kernel (device-side count).
-int launch_csr_pairs(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
-    void* scratch = nullptr;
-    const size_t bytes = lnl::pair_prep_scratch_words(a.n) * sizeof(uint32_t);
-    hipError_t e = hipMallocAsync(&scratch, bytes, st);
-    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
-    lnl::PairPrepArgs p{};
-    p.base = a.base;
-    p.off = a.off;
-    p.off0 = a.off0;
-    p.n = a.n;
-    lnl::pair_prep_layout(p, (uint32_t*)scratch);
-    int rc = 0;
-    e = lnl::launch_pair_prep(p, st);
-    if (e != hipSuccess) rc = hip_fail(e, "pair pre-pass launch");
-    if (rc == 0) {
-        lnl::PairArgs q{};
-        q.base = a.base;
-        q.n = a.n;
-        q.out = a.out;
-        q.fold = S.fold;
-        q.desc = p.desc;
-        q.ctl = p.ctl;
-        const uint32_t waves_max = (a.n / 2u + 1u) / 64u + 1u + lnl::kPairKeys;
-        const uint32_t per_wg = lnl::kPairThreads / 64;
-        const int grid = (int)std::max(1u, std::min((waves_max + per_wg - 1) / per_wg, (uint32_t)S.cus));
-        e = lnl::launch_crc32c_pair(q, grid, st);
-        if (e != hipSuccess) rc = hip_fail(e, "pair kernel launch");
-    }
-    if (rc == 0) {
-        lnl::BatchArgs o = a;
-        o.perm = p.ovf;
-        o.perm_n = p.ctl + 1;
-        rc = launch(S, o, lnl::kModeCsr, st);
-    }
-    e = hipFreeAsync(scratch, st);
-    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
-    return rc;
-}
-
-// CSR batches: the segment kernel (crc32c_seg.hip: every line read once)
-// after its pre-pass, then the batch kernel over the datagrams it leaves
-// (device-side count).
-int launch_csr_seg(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
-    lnl::SegArgs g{};
-    g.base = a.base;
-    g.off = a.off;
-    g.off0 = a.off0;
-    g.n = a.n;
-    g.waves = (uint32_t)S.cus * (uint32_t)(lnl::kSegThreads / 64);
-    g.out = a.out;
-    g.fold = S.fold;
-    g.pow = S.pow;
-    void* scratch = nullptr;
-    const size_t bytes = lnl::seg_scratch_words(a.n, g.waves) * sizeof(uint32_t);
-    hipError_t e = hipMallocAsync(&scratch, bytes, st);
-    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
-    lnl::seg_scratch_layout(g, (uint32_t*)scratch);
-    int rc = 0;
-    e = lnl::launch_seg(g, S.cus, st);
-    if (e != hipSuccess) rc = hip_fail(e, "segment kernel launch");
-    if (rc == 0) {
-        lnl::BatchArgs o = a;
-        o.perm = g.ovf;
-        o.perm_n = g.ctl + 1;
-        rc = launch(S, o, lnl::kModeCsr, st);
-    }
-    e = hipFreeAsync(scratch, st);
-    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
-    return rc;
-}
-
-// CSR batches: the uniform path (crc32c_csr.hip), then the batch kernel over
-// its overflow datagrams, which also XORs the shared-line tail contributions
-// into out.
-int launch_csr_uniform(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st) {
-    void* scratch = nullptr;
-    const size_t bytes = lnl::csr_plan_scratch_words(a.n) * sizeof(uint32_t);
-    hipError_t e = hipMallocAsync(&scratch, bytes, st);
-    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
-    lnl::CsrPlanArgs p{};
-    p.base = a.base;
-    p.off = a.off;
-    p.off0 = a.off0;
-    p.n = a.n;
-    p.out = a.out;
-    lnl::csr_plan_layout(p, (uint32_t*)scratch);
-    lnl::CsrArgs c{};
-    c.base = a.base;
-    c.desc = p.desc;
-    c.ctl = p.ctl;
-    c.out = a.out;
-    c.tail = p.tail;
-    c.dummy = S.dummy;
-    c.fold = S.fold;
-    c.amat = S.pow;  // table 0 = A^(2^0)
-    // batches <= n / 64 + one partial batch per key
-    const uint32_t waves_max = a.n / 64u + lnl::kBuckets;
-    int rc = 0;
-    e = lnl::launch_csr_uniform(p, c, grid_for_waves(S, waves_max, 512), st);  // kThreads of crc32c_csr.hip
-    if (e != hipSuccess) rc = hip_fail(e, "CSR uniform launch");
-    if (rc == 0) {
-        lnl::BatchArgs o = a;
-        o.perm = p.ovf;
-        o.perm_n = p.ctl + 1;
-        o.tail_xor = p.tail;
-        o.xor_n = a.n;
-        rc = launch(S, o, lnl::kModeCsr, st);
-    }
-    e = hipFreeAsync(scratch, st);
-    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
-    return rc;
-}
 #endif  // LNL_EXPERIMENTS
 
 #ifndef LNL_SPAN_ROUNDS
@@ -504,16 +380,6 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
 int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
     if (a.n < LNL_BUCKET_MIN_N) return launch(S, a, mode, st);
     if (mode == lnl::kModeCsr && csr_path() == kPathBucketed) return launch_csr_span(S, a, st);
-#if LNL_EXPERIMENTS
-    if (mode == lnl::kModeCsr) {
-        switch (csr_path()) {
-            case kPathUniform: return launch_csr_uniform(S, a, st);
-            case kPathSeg: return launch_csr_seg(S, a, st);
-            case kPathPairs: return launch_csr_pairs(S, a, st);
-            default: break;
-        }
-    }
-#endif
     void* scratch = nullptr;
     const size_t bytes = lnl::bucket_scratch_words(a.n) * sizeof(uint32_t);
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
@@ -603,7 +469,7 @@ extern "C" int lnl_crc32c_abi_version(void) { return LNL_CRC32C_ABI_VERSION; }
 // kernel, 1 uniform, 2 segment, 3 pair; see csr_path above).  Returns the
 // previous path, or -EINVAL.
 extern "C" int lnl_crc32c_set_csr_path(int path) {
-    if (path < kPathBucketed || path > kPathBucketCsr) return fail(-EINVAL, "CSR path %d out of range", path);
+    if (path != kPathBucketed && path != kPathBucketCsr) return fail(-EINVAL, "CSR path %d not built", path);
     const int prev = csr_path();
     g_csr_path.store(path);
     return prev;
@@ -736,38 +602,7 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
     // the bucketed batch kernel, which computes them
     if (n >= LNL_BUCKET_MIN_N && !d_crc && path == kPathBucketed)
         return launch_csr_span(*S, a, st, filter ? lnl::kSpanFilter : lnl::kSpanVerify);
-    if (n < LNL_BUCKET_MIN_N || path == kPathBucketed || path == kPathBucketCsr)
-        return launch_csr(*S, a, lnl::kModeVerify, st);
-#if !LNL_EXPERIMENTS
-    return fail(-EINVAL, "unreachable CSR path %d", path);
-#else
-    // large batches on an experiment path: CRCs of the whole wire datagrams
-    // with that path's kernel, then ok / body CRC per datagram (crc32c_verify.hip)
-    void* wire = nullptr;
-    hipError_t e = hipMallocAsync(&wire, (size_t)n * 4u, st);
-    if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync: %s", hipGetErrorString(e));
-    lnl::BatchArgs w = a;
-    w.out = (uint32_t*)wire;
-    w.ok = nullptr;
-    int rc = path == kPathSeg ? launch_csr_seg(*S, w, st)
-             : path == kPathPairs ? launch_csr_pairs(*S, w, st)
-                                  : launch_csr_uniform(*S, w, st);
-    if (rc == 0) {
-        lnl::VerifyArgs v{};
-        v.base = d_base;
-        v.off = d_off;
-        v.n = n;
-        v.wire = (const uint32_t*)wire;
-        v.ok = d_ok;
-        v.crc = d_crc;
-        v.filter = filter;
-        e = lnl::launch_verify_from_wire(v, st);
-        if (e != hipSuccess) rc = hip_fail(e, "verify epilogue launch");
-    }
-    e = hipFreeAsync(wire, st);
-    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
-    return rc;
-#endif
+    return launch_csr(*S, a, lnl::kModeVerify, st);
 }
 }  // namespace
 

@@ -93,76 +93,6 @@ size_t bucket_scratch_words(uint32_t n);
 void bucket_layout(BucketArgs& a, uint32_t* scratch);
 hipError_t launch_csr_buckets(const BucketArgs& a, hipStream_t stream);
 
-// CSR pair kernel (crc32c_pair.hip) and its pre-pass.  Item j = datagrams
-// (2j, 2j+1); key = (Ta, Tb, shared) with Ta, Tb <= kPairMaxT, else overflow
-// (both datagrams go to the batch kernel through `ovf`).  perm lists items
-// key by key, each key's group padded with kPairIdle to a multiple of 64.
-constexpr uint32_t kPairMaxT = 15;
-constexpr uint32_t kPairKeys = (kPairMaxT + 1) * (kPairMaxT + 1) * 2;  // 512
-constexpr uint32_t kPairIdle = 0xFFFFFFFFu;
-
-struct PairPrepArgs {
-    const uint8_t* base;
-    const uint64_t* off;
-    uint64_t off0;
-    uint32_t n;         // datagrams; items = (n + 1) / 2
-    uint32_t* counts;   // kPairKeys + 1 (last: overflow items)
-    uint32_t* fill;     // kPairKeys
-    uint32_t* bases;    // kPairKeys: start of each key's group in perm
-    uint32_t* ctl;      // [0] = wave-batches (desc entries / 64), [1] = overflow datagrams
-    uint4* desc;        // items + 64 * kPairKeys pair descriptors (see PairArgs)
-    uint32_t* ovf;      // n entries
-};
-
-// Zeroes the counters, then count / bases+padding / scatter kernels.
-hipError_t launch_pair_prep(const PairPrepArgs& a, hipStream_t stream);
-size_t pair_prep_scratch_words(uint32_t n);
-void pair_prep_layout(PairPrepArgs& a, uint32_t* scratch);
-
-// Pair descriptor, written by the pre-pass in bucket order, one per lane:
-//   x: line index of the run's first line, counted from base's line
-//   y: pad_a | be_a << 8 | pad_b << 16 | be_b << 24 (offsets of a's / b's
-//      first and last byte in their first / last line)
-//   z: datagram a (b = a + 1); n marks a padding (idle) entry
-//   w: (b < n) | key << 8, key = (Ta * (kPairMaxT + 1) + Tb) * 2 + shared
-struct PairArgs {
-    const uint8_t* base;
-    uint32_t n;
-    uint32_t* out;
-    const uint32_t* fold;
-    const uint4* desc;
-    const uint32_t* ctl;  // device, from the pre-pass: [0] wave-batches, [3] last line of the buffer
-};
-
-constexpr int kPairThreads = 512;  // one workgroup (8 waves) per CU
-hipError_t launch_crc32c_pair(const PairArgs& a, int grid, hipStream_t stream);
-
-// CSR segment kernel (crc32c_seg.hip): every line of the batch read once, lane
-// g owns the datagrams ending in segment g (crc32c_seg.h).  launch_seg enqueues
-// the counter reset, the pre-pass, the kernel and the cross-wave fix-up; the
-// caller then runs the batch kernel over ovf (perm_n = ctl + 1).
-constexpr int kSegThreads = 512;  // one workgroup (8 waves) per CU
-struct SegArgs {
-    const uint8_t* base;
-    const uint64_t* off;
-    uint64_t off0;
-    uint32_t n;
-    uint32_t waves;         // resident waves of the kernel's grid (CUs x 8)
-    uint32_t* out;
-    const uint32_t* fold;   // LNL_TABLE_WORDS words (lnl_build_tables)
-    const uint32_t* pow;    // kSegPowTables x 128 words (lnl_build_seg_tables)
-    uint32_t* ctl;          // 4 words: [1] overflow datagrams
-    uint32_t* first;        // seg_max_segments(waves) + 1
-    uint32_t* ovf;          // n: datagrams left to the batch kernel
-    uint32_t* carry;        // seg_max_segments(waves) / 64: each wave-batch's lane-63 tail
-    uint4* fix;             // same count: each wave-batch's lane-0 head
-};
-
-hipError_t launch_seg(const SegArgs& a, int grid, hipStream_t stream);
-// scratch words (u32) launch_seg needs for n datagrams on `waves` resident waves
-size_t seg_scratch_words(uint32_t n, uint32_t waves);
-void seg_scratch_layout(SegArgs& a, uint32_t* scratch);
-
 // CSR span path (crc32c_span.hip): every line of the stream read once, lane
 // g owns segment g; datagram folds batched wave-uniformly through an LDS
 // stash.  launch_span enqueues the pre-pass and the kernel;
@@ -208,39 +138,6 @@ struct AppendArgs {
     uint64_t off0;  // datagram i's bytes are base[off[i] - off0 ..) (host-path chunks: off0 = off[0])
 };
 hipError_t launch_append(const AppendArgs& a, int cus, hipStream_t stream);
-
-// CSR uniform path (crc32c_csr.hip): plan pre-pass + uniform line-count
-// batches that fetch each shared boundary line once.  The caller then runs
-// the batch kernel over ovf (perm_n = ctl + 1) with tail_xor = tail.
-constexpr uint32_t kCsrMaxRows = 63;  // longer datagrams (> 8 KiB) go to the batch kernel
-constexpr uint64_t kCsrMaxLine = (1u << 25) - 64u;  // and those starting >= ~4 GiB after base
-struct CsrPlanArgs {
-    const uint8_t* base;
-    const uint64_t* off;
-    uint64_t off0;
-    uint32_t n;
-    uint32_t* out;     // CRC 0 for empty datagrams
-    uint32_t* counts;  // kBucketCounterWords (counts + fill), then ctl
-    uint32_t* fill;
-    uint32_t* ctl;     // [0] uniform batches, [1] overflow datagrams
-    uint4* desc;       // n + 64 * kBuckets entries
-    uint32_t* tail;    // n: tail contribution of datagram i (0 unless it drops its last line)
-    uint32_t* ovf;     // n: overflow datagrams
-};
-struct CsrArgs {
-    const uint8_t* base;
-    const uint4* desc;
-    const uint32_t* ctl;
-    uint32_t* out;
-    uint32_t* tail;
-    const uint8_t* dummy;
-    const uint32_t* fold;  // LNL_TABLE_WORDS (lnl_build_tables)
-    const uint32_t* amat;  // 128 words: A as nibble tables (lnl_build_seg_tables, table 0)
-};
-size_t csr_plan_scratch_words(uint32_t n);
-void csr_plan_layout(CsrPlanArgs& a, uint32_t* scratch);
-// zeroes the counters, then plan count / plan scatter / uniform kernel
-hipError_t launch_csr_uniform(const CsrPlanArgs& p, const CsrArgs& c, int grid, hipStream_t stream);
 
 // XOR-encryption layer over a batch (lnl_xor.hip), in place.
 constexpr uint32_t kXorMaxKey = 256;
@@ -313,19 +210,5 @@ hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_by
 // accepted; walking again only what the blocks cannot hold), then scan + emit
 // as above.
 hipError_t launch_dispatch_walked(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
-
-// Verify epilogue (crc32c_verify.hip): ok / body CRC from wire-datagram CRCs.
-struct VerifyArgs {
-    const uint8_t* base;
-    const uint64_t* off;
-    uint64_t off0;
-    uint32_t n;
-    const uint32_t* wire;  // CRC-32C of each whole datagram
-    uint8_t* ok;
-    uint32_t filter;       // as BatchArgs::filter
-    uint32_t* crc;         // optional
-};
-
-hipError_t launch_verify_from_wire(const VerifyArgs& a, hipStream_t stream);
 
 }  // namespace lnl

@@ -82,17 +82,8 @@ VARIANTS = {
     "k16": "-DLNL_RUN_K=16",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
     "run_late": "-DLNL_RUN_EARLY_ROWS=0",           # run kernel: first rows issued after the tables land (before round 3)
-    # CSR experiment paths: same library, runtime path (lnl_crc32c_set_csr_path)
-    "uniform": ("", 1),                             # CSR: uniform line-count batches, shared lines once
-    "seg": ("", 2),                                 # CSR: segment kernel
-    "pairs": ("", 3),                               # CSR: pair kernel
-    "seg_nofold": ("-DLNL_SEG_DIAG_NOFOLD", 2),     # segment kernel without its folds (wrong CRCs): their cost
+    # (round 1's uniform / segment / pair CSR paths: tools/experiments/csr_experiment_kernels.patch)
     "nobucket": "-DLNL_BUCKET_MIN_N=0xFFFFFFFFu",   # CSR: plain batch kernel, no pre-pass
-    "csr_edge_nt": ("-DLNL_CSR_EDGE_AUX=2", 1),     # uniform kernel: nt for rows 0 / R-1 too
-    "csr_dflt": ("-DLNL_CSR_AUX=0", 1),             # uniform kernel: default policy for the middle rows
-    "csr_memonly": ("-DLNL_CSR_DIAG_MEMONLY", 1),   # uniform kernel, rows loaded and read only (wrong CRCs)
-    "pair_edge_nt": ("-DLNL_PAIR_EDGE_AUX=2", 3),   # pair kernel: nt for the shared-line fetches too
-    "pair_dflt": ("-DLNL_PAIR_AUX=0", 3),           # pair kernel: default policy for every fetch
     "bucket_atomic": "-DLNL_BUCKET_LAYOUT=0",       # CSR: atomic ranks, bucket after bucket (16 runs per bucket)
     "bucket_interleave": "-DLNL_BUCKET_LAYOUT=1",   # CSR: position-ordered buckets, batches interleaved by progress
     "xor_dflt": "-DLNL_XOR_NT=0",                   # XOR layer: default policy loads / stores
