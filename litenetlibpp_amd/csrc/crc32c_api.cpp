@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/lnl_crc32c.h"
+#include "crc32c_append.h"
 #include "crc32c_bitslice.h"
 #include "crc32c_kernels.h"
 #include "crc32c_seg.h"
@@ -80,6 +81,7 @@ struct DeviceState {
     uint32_t* fold = nullptr;  // kernel tables (lnl_build_tables), 12.5 KiB
     uint32_t* pow = nullptr;   // segment kernel's row-power tables (lnl_build_seg_tables), 3.5 KiB
     uint32_t* span_tab = nullptr;  // span kernel's tables (lnl_build_span_tables), 145 KiB
+    uint32_t* append_tab = nullptr;  // outbound layer's tables (lnl_build_append_tables), 104 KiB
     int cus = 0;
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)
@@ -113,11 +115,13 @@ int device_state(int dev, DeviceState** out) {
         static uint32_t host_fold[LNL_TABLE_WORDS];
         static uint32_t host_pow[lnl::kSegPowTables * 128];
         static uint32_t host_span[lnl::kSpanTabWords];
+        static uint32_t host_app[lnl::kAppTabWords];
         static std::once_flag fold_once;
         std::call_once(fold_once, [] {
             lnl_build_tables(host_fold);
             lnl_build_seg_tables(host_pow, (int)lnl::kSegPowTables);
             lnl::lnl_build_span_tables(host_span);
+            lnl::lnl_build_append_tables(host_app);
         });
         e = hipMalloc(&S.dummy, 256);
         if (e == hipSuccess) e = hipMemset(S.dummy, 0, 256);
@@ -127,6 +131,8 @@ int device_state(int dev, DeviceState** out) {
         if (e == hipSuccess) e = hipMemcpy(S.pow, host_pow, sizeof host_pow, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&S.span_tab, sizeof host_span);
         if (e == hipSuccess) e = hipMemcpy(S.span_tab, host_span, sizeof host_span, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc(&S.append_tab, sizeof host_app);
+        if (e == hipSuccess) e = hipMemcpy(S.append_tab, host_app, sizeof host_app, hipMemcpyHostToDevice);
         // CSR / verify calls take their scratch from the stream-ordered pool
         // (hipMallocAsync / hipFreeAsync on the caller's stream).  Keep freed
         // blocks in the pool across synchronisations: with the default
@@ -528,23 +534,24 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
 }  // namespace
 
 namespace {
-// The outbound layer over a device burst whose CRCs go to crc (n words): the
-// CSR CRC pass, then the append kernel (lnl_append.hip).
+// The outbound layer over a device burst: the one-pass append kernel
+// (lnl_append.hip), CRCs into crc when it is not null.  (The experiments
+// build's two-pass form runs the CSR CRC pass into crc first.)
 int append_csr(const DeviceState& S, const lnl::BatchArgs& src, uint8_t* d_dst, uint32_t* crc, hipStream_t st) {
-    lnl::BatchArgs a = src;
-    a.out = crc;
-    int rc = launch_csr(S, a, lnl::kModeCsr, st);
-    if (rc == 0) {
-        lnl::AppendArgs p{a.base, a.off, a.n, d_dst, crc, a.off0};
-        hipError_t e = lnl::launch_append(p, S.cus, st);
-        if (e != hipSuccess) rc = hip_fail(e, "append kernel launch");
+    if (lnl::append_two_pass()) {
+        if (!crc) return fail(-EINVAL, "the two-pass append needs a CRC buffer");
+        lnl::BatchArgs a = src;
+        a.out = crc;
+        if (int rc = launch_csr(S, a, lnl::kModeCsr, st)) return rc;
     }
-    return rc;
+    lnl::AppendArgs p{src.base, src.off, src.n, d_dst, crc, src.off0, S.append_tab};
+    hipError_t e = lnl::launch_append(p, S.cus, st);
+    return e == hipSuccess ? 0 : hip_fail(e, "append kernel launch");
 }
 }  // namespace
 
-// The outbound layer over a device burst: the CSR CRC pass (into d_crc, or
-// stream-ordered scratch), then the append kernel (lnl_append.hip).
+// The outbound layer over a device burst: one pass over the payload bytes
+// (lnl_append.hip), the CRCs into d_crc when it is not null.
 extern "C" int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t* d_dst,
                                          uint32_t* d_crc, void* hip_stream) {
     if (n == 0) return 0;
@@ -554,7 +561,8 @@ extern "C" int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* 
     if (int rc = current_device(&S)) return rc;
     const hipStream_t st = (hipStream_t)hip_stream;
     uint32_t* crc = d_crc;
-    if (!crc) {
+    const bool scratch = !crc && lnl::append_two_pass();
+    if (scratch) {
         hipError_t e = hipMallocAsync((void**)&crc, (size_t)n * sizeof(uint32_t), st);
         if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", (size_t)n * 4, hipGetErrorString(e));
     }
@@ -563,7 +571,7 @@ extern "C" int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* 
     a.off = d_off;
     a.n = n;
     int rc = append_csr(*S, a, d_dst, crc, st);
-    if (!d_crc) {
+    if (scratch) {
         hipError_t e = hipFreeAsync(crc, st);
         if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
     }

@@ -48,12 +48,6 @@ namespace {
 #endif
 
 constexpr int kThreads = 256;
-#if LNL_EXPERIMENTS
-constexpr int kPerThread = 16;                    // pair count pass
-constexpr uint32_t kPerBlock = kThreads * kPerThread;
-constexpr int kScatterPerThread = 16;             // pair scatter pass
-constexpr uint32_t kScatterPerBlock = kThreads * kScatterPerThread;
-#endif
 constexpr int kBucketPerThread = 4;               // bucket count and scatter passes
 constexpr uint32_t kBucketPerBlock = kThreads * kBucketPerThread;
 
@@ -369,174 +363,8 @@ __global__ __launch_bounds__(kWinThreads) void bucket_window_kernel(BucketArgs a
 }
 static_assert(kBuckets == 64, "bucket_window_kernel scans the counts with one wave");
 
-#if LNL_EXPERIMENTS
-// ---- pairs (crc32c_pair.hip; experiments build only) ------------------------
-
-// Key of item j (kPairKeys: overflow) and, for the scatter, its descriptor.
-__device__ inline uint32_t pair_key(const PairPrepArgs& a, uint32_t j, uint4* d = nullptr) {
-    const uint32_t ia = 2u * j;
-    const bool hasb = ia + 1u < a.n;
-    const uint64_t s0 = a.off[ia], s1 = a.off[ia + 1u];
-    const uint64_t s2 = hasb ? a.off[ia + 2u] : s1;
-    const uint64_t la = s1 - s0, lb = s2 - s1;
-    const uint64_t abs_a = (uint64_t)(uintptr_t)a.base + (s0 - a.off0), abs_b = abs_a + la;
-    const uint64_t Ta = la ? ((abs_a + la - 1u) >> 7) - (abs_a >> 7) + 1u : 0u;
-    const uint64_t Tb = lb ? ((abs_b + lb - 1u) >> 7) - (abs_b >> 7) + 1u : 0u;
-    if (Ta > kPairMaxT || Tb > kPairMaxT) return kPairKeys;  // overflow
-    const uint32_t sh = (la && lb && ((abs_a + la - 1u) >> 7) == (abs_b >> 7)) ? 1u : 0u;
-    const uint32_t key = ((uint32_t)Ta * (kPairMaxT + 1u) + (uint32_t)Tb) * 2u + sh;
-    if (d) {
-        const uint64_t first = la ? abs_a : abs_b;
-        d->x = (uint32_t)((first >> 7) - ((uint64_t)(uintptr_t)a.base >> 7));
-        d->y = ((uint32_t)abs_a & 127u) | (((uint32_t)(abs_a + la - 1u) & 127u) << 8) |
-               (((uint32_t)abs_b & 127u) << 16) | (((uint32_t)(abs_b + lb - 1u) & 127u) << 24);
-        d->z = ia;
-        d->w = (hasb ? 1u : 0u) | (key << 8);
-    }
-    return key;
-}
-
-__global__ __launch_bounds__(kThreads) void pair_count_kernel(PairPrepArgs a) {
-    constexpr int kW = kThreads / 64;
-    constexpr uint32_t kBins = kPairKeys + 1u;
-    __shared__ uint32_t hist[kW][kBins];
-    for (uint32_t k = threadIdx.x; k < kW * kBins; k += kThreads) (&hist[0][0])[k] = 0;
-    __syncthreads();
-    const uint32_t items = (a.n + 1u) / 2u;
-    const uint32_t j0 = blockIdx.x * kPerBlock + threadIdx.x;
-    uint32_t key[kPerThread];
-#pragma unroll
-    for (int r = 0; r < kPerThread; ++r) {
-        const uint32_t j = j0 + r * kThreads;
-        key[r] = j < items ? pair_key(a, j) : kBins;
-    }
-    uint32_t* h = hist[threadIdx.x >> 6];
-#pragma unroll
-    for (int r = 0; r < kPerThread; ++r)
-        if (key[r] < kBins) atomicAdd(&h[key[r]], 1u);
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kBins; k += kThreads) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int w = 0; w < kW; ++w) c += hist[w][k];
-        if (c) atomicAdd(&a.counts[k], c);
-    }
-}
-
-// Scatter.  Every workgroup first derives the group starts itself (each
-// key's count rounded up to 64, exclusive scan over the 512 keys in LDS);
-// workgroup 0 also writes the padding entries (idle lanes carrying the
-// group's key), the wave-batch count and the buffer's last line.
-__global__ __launch_bounds__(kThreads) void pair_scatter_kernel(PairPrepArgs a) {
-    static_assert(kPairKeys == 2 * kThreads, "two keys per thread");
-    constexpr uint32_t kBins = kPairKeys + 1u;
-    __shared__ uint32_t hist[kBins], base[kBins], gstart[kPairKeys], part[kThreads];
-    const uint32_t t = threadIdx.x;
-    for (uint32_t k = t; k < kBins; k += kThreads) hist[k] = 0;
-    {
-        const uint32_t c0 = a.counts[2 * t], c1 = a.counts[2 * t + 1];
-        const uint32_t p0 = (c0 + 63u) & ~63u, p1 = (c1 + 63u) & ~63u;
-        part[t] = p0 + p1;
-        __syncthreads();
-        for (uint32_t d = 1; d < kThreads; d <<= 1) {  // Hillis-Steele inclusive scan
-            const uint32_t v = t >= d ? part[t - d] : 0u;
-            __syncthreads();
-            part[t] += v;
-            __syncthreads();
-        }
-        const uint32_t excl = part[t] - (p0 + p1);
-        gstart[2 * t] = excl;
-        gstart[2 * t + 1] = excl + p0;
-        if (blockIdx.x == 0) {
-            if (t == kThreads - 1) a.ctl[0] = part[t] / 64u;
-            if (t == 0) {  // last line of the buffer (the pair kernel clamps its fetches to it)
-                const uint64_t bytes = a.off[a.n] - a.off0;
-                const uint64_t b = (uint64_t)(uintptr_t)a.base;
-                a.ctl[3] = bytes ? (uint32_t)(((b + bytes - 1u) >> 7) - (b >> 7)) : 0u;
-            }
-        }
-        __syncthreads();
-        if (blockIdx.x == 0) {
-            for (uint32_t idx = t; idx < kPairKeys * 64u; idx += kThreads) {
-                const uint32_t k = idx >> 6, p = idx & 63u;
-                const uint32_t c = a.counts[k];
-                if ((c & 63u) != 0u && p >= (c & 63u))
-                    a.desc[gstart[k] + (c & ~63u) + p] = make_uint4(0u, 0u, a.n, k << 8);
-            }
-        }
-    }
-    const uint32_t items = (a.n + 1u) / 2u;
-    const uint32_t j0 = blockIdx.x * kScatterPerBlock + threadIdx.x;
-    uint32_t key[kScatterPerThread], rank[kScatterPerThread];
-    uint4 d[kScatterPerThread];
-#pragma unroll
-    for (int r = 0; r < kScatterPerThread; ++r) {
-        const uint32_t j = j0 + r * kThreads;
-        key[r] = j < items ? pair_key(a, j, &d[r]) : 0u;
-    }
-#pragma unroll
-    for (int r = 0; r < kScatterPerThread; ++r) {
-        const uint32_t j = j0 + r * kThreads;
-        rank[r] = j < items ? atomicAdd(&hist[key[r]], 1u) : 0u;
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kBins; k += kThreads) {
-        const uint32_t h = hist[k];
-        if (k < kPairKeys)
-            base[k] = gstart[k] + (h ? atomicAdd(&a.fill[k], h) : 0u);
-        else if (h)  // overflow items: 2 datagram slots each in ovf
-            base[k] = atomicAdd(&a.ctl[2], h), atomicAdd(&a.ctl[1], 2u * h);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kScatterPerThread; ++r) {
-        const uint32_t j = j0 + r * kThreads;
-        if (j >= items) continue;
-        if (key[r] < kPairKeys) {
-            a.desc[base[key[r]] + rank[r]] = d[r];
-        } else {
-            const uint32_t pos = 2u * (base[kPairKeys] + rank[r]);
-            a.ovf[pos] = 2u * j;
-            a.ovf[pos + 1u] = 2u * j + 1u < a.n ? 2u * j + 1u : 0xFFFFFFFFu;  // idle lane
-        }
-    }
-}
-
-#endif  // LNL_EXPERIMENTS
 }  // namespace
 
-#if LNL_EXPERIMENTS
-size_t pair_prep_scratch_words(uint32_t n) {
-    const size_t items = ((size_t)n + 1) / 2;
-    return (kPairKeys + 1) + kPairKeys + 4 + kPairKeys + 4 * (items + 64 * (size_t)kPairKeys) + ((size_t)n + 1) + 4;
-}
-
-void pair_prep_layout(PairPrepArgs& a, uint32_t* w) {
-    const size_t items = ((size_t)a.n + 1) / 2;
-    a.counts = w;
-    a.fill = a.counts + (kPairKeys + 1);
-    a.ctl = a.fill + kPairKeys;  // 4 words: [0] wave-batches, [1] ovf entries, [2] ovf items, [3] last line
-    a.bases = a.ctl + 4;
-    uint32_t* d = a.bases + kPairKeys;
-    d += (4 - ((uintptr_t)d / 4) % 4) % 4;  // 16-byte alignment
-    a.desc = (uint4*)d;
-    a.ovf = d + 4 * (items + 64 * (size_t)kPairKeys);
-}
-
-hipError_t launch_pair_prep(const PairPrepArgs& a, hipStream_t stream) {
-    // counts, fill and ctl are contiguous
-    hipError_t e = hipMemsetAsync(a.counts, 0, ((kPairKeys + 1) + kPairKeys + 4) * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
-    const uint32_t items = (a.n + 1u) / 2u;
-    hipLaunchKernelGGL(pair_count_kernel, dim3((items + kPerBlock - 1) / kPerBlock), dim3(kThreads), 0, stream, a);
-    hipLaunchKernelGGL(pair_scatter_kernel, dim3((items + kScatterPerBlock - 1) / kScatterPerBlock),
-                       dim3(kThreads), 0, stream, a);
-    return hipGetLastError();
-}
-
-
-
-#endif  // LNL_EXPERIMENTS
 
 // Descriptor layout of the product build: windows of 2048 datagrams sorted by
 // line count, 256-thread workgroups, placed in 4 sweeps.  The

@@ -31,23 +31,13 @@ VARIANTS = {
     "run512p": "-DLNL_RUN_THREADS=512 -DLNL_RUN_PRIO=1",  # ... with progress-based issue priority
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
     "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
-    "app_t64": "-DLNL_APPEND_TEAM=64",              # append kernel: 64 lanes per datagram (default 32)
-    "app_t16": "-DLNL_APPEND_TEAM=16",
-    "app_nts": "-DLNL_APPEND_NT=1",                 # append kernel: nontemporal chunk stores
-    "app_ntl": "-DLNL_APPEND_NT=2",                 # ... loads
-    "app_nt": "-DLNL_APPEND_NT=3",                  # ... both
-    "app_scdf": "-DLNL_APPEND_STORE_SFX=\\\"\\\"",   # append kernel: chunk stores with the default policy (the product)
-    "app_u2": "-DLNL_APPEND_UNROLL=2",   # append kernel: the chunk loop unrolled twice around the asm store
-    "app_blk": "-DLNL_APPEND_BLOCKED=1",   # append kernel: each team owns a run of consecutive datagrams
-    "app_sc1": "-DLNL_APPEND_STORE_SFX=\\\"sc1\\\"",   # append kernel: chunk stores with cache-policy bits
-    "app_sc01": "-DLNL_APPEND_STORE_SFX=\\\"sc0\\ sc1\\\"",
-    "app_sc0": "-DLNL_APPEND_STORE_SFX=\\\"sc0\\\"",
-    "app_w4": "-DLNL_APPEND_WGS=4u",                # append kernel: 4 / 8 / 32 workgroups per CU (default 16)
-    "app_w8": "-DLNL_APPEND_WGS=8u",
-    "app_w32": "-DLNL_APPEND_WGS=32u",
-    "app_nohead": "-DLNL_APPEND_DIAG=1",            # append kernel: no head / tail byte stores (wrong burst)
-    "app_nochunk": "-DLNL_APPEND_DIAG=2",           # ... no chunk stores (wrong burst)
-    "app_nostore": "-DLNL_APPEND_DIAG=3",           # ... no stores at all (wrong burst)
+    "app_2pass": "-DLNL_APPEND_TWO_PASS=1",          # outbound layer: round 3's CSR CRC pass + copy kernel
+    "app_r16": "-DLNL_APP_REPL=16",                 # one-pass append: lane tables in 16 copies (2-way bank sharing)
+    "app_r8": "-DLNL_APP_REPL=8",
+    "app_s16": "-DLNL_APP_SLICE16=1",               # one-pass append: slicing-by-16 piece CRC (16 independent lookups)
+    "app_g2": "-DLNL_APPEND_GROUP=2",               # one-pass append: pieces per lane loaded together (default 3)
+    "app_g4": "-DLNL_APPEND_GROUP=4",
+    "app_t512": "-DLNL_APPEND_THREADS=512",         # one-pass append: 512-thread workgroups (8 waves per CU)
     "prep8k": "-DLNL_SPAN_PREP_BLOCKS=8192u",       # span pre-pass: 8192 workgroups (before: 1 % slower than 1024)
     "prep256": "-DLNL_SPAN_PREP_BLOCKS=256u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
