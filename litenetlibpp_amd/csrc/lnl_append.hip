@@ -28,8 +28,9 @@
 #include "crc32c_device.h"
 #include "crc32c_kernels.h"
 
-#ifndef LNL_APPEND_TWO_PASS
-#define LNL_APPEND_TWO_PASS 0  // experiments build only: the round-3 form (CSR CRC pass + copy kernel)
+#ifndef LNL_APPEND_MODE
+#define LNL_APPEND_MODE 0  // 0: CSR CRC pass + the copy kernel (the product); experiments build only:
+                           // 1 one pass (the team computes the CRCs), 2 CSR CRC pass + the team copy
 #endif
 
 namespace lnl {
@@ -47,8 +48,7 @@ struct __attribute__((packed, aligned(4))) U4a {  // 16 bytes at a 4-byte aligne
 #ifndef LNL_APPEND_THREADS
 #define LNL_APPEND_THREADS 1024
 #endif
-constexpr int kThreads = LNL_APPEND_THREADS;
-constexpr uint32_t kTeamsPerWg = kThreads / kAppTeam;
+[[maybe_unused]] constexpr int kThreads = LNL_APPEND_THREADS;  // the one-pass form's workgroup
 #ifndef LNL_APPEND_GROUP
 #define LNL_APPEND_GROUP 3  // pieces per lane loaded before any is folded (3: a 1,536-byte datagram at once)
 #endif
@@ -85,16 +85,31 @@ __device__ LNL_INLINE void load_dwords(uint64_t sa, uint64_t lo, uint64_t hi, ui
 }
 
 // bytes kept of the 4 at [4 m, 4 m + 4) of a piece whose payload is [lo, hi)
-__device__ LNL_INLINE uint32_t keep_word(int32_t lo, int32_t hi, uint32_t m) {
+[[maybe_unused]] __device__ LNL_INLINE uint32_t keep_word(int32_t lo, int32_t hi, uint32_t m) {
     auto low = [](int32_t b) -> uint32_t { return b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : (1u << (8 * b)) - 1u); };
     return low(hi - 4 * (int32_t)m) & ~low(lo - 4 * (int32_t)m);
 }
 
-__global__ __launch_bounds__(kThreads, 1) void append_crc_kernel(AppendArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t T[kAppTabWords];
-    for (uint32_t i = threadIdx.x; i < kAppTabWords / 4; i += kThreads)
-        reinterpret_cast<uint4*>(T)[i] = reinterpret_cast<const uint4*>(a.tab)[i];
-    __syncthreads();
+#ifndef LNL_APPEND_COPY_THREADS
+#define LNL_APPEND_COPY_THREADS 256
+#endif
+#ifndef LNL_APPEND_COPY_WGS
+#define LNL_APPEND_COPY_WGS 8  // copy kernel: workgroups per CU (persistent grid)
+#endif
+[[maybe_unused]] constexpr int kCopyTeamThreads = LNL_APPEND_COPY_THREADS;
+
+// CRC: the one-pass form (the team computes each datagram's CRC from the
+// pieces it copies; LDS tables); otherwise the copy after the CSR CRC pass
+// (a.crc in), the same pieces, ownership rule and tail-chunk assembly.
+template <bool CRC, int THREADS>
+__global__ __launch_bounds__(THREADS, CRC ? 1 : 2) void append_team_kernel(AppendArgs a) {
+    constexpr uint32_t kTeamsPerWg = THREADS / kAppTeam;
+    __shared__ __attribute__((aligned(16))) uint32_t T[CRC ? kAppTabWords : 4];
+    if constexpr (CRC) {
+        for (uint32_t i = threadIdx.x; i < kAppTabWords / 4; i += THREADS)
+            reinterpret_cast<uint4*>(T)[i] = reinterpret_cast<const uint4*>(a.tab)[i];
+        __syncthreads();
+    }
 
     const uint32_t q = threadIdx.x % kAppTeam;  // lane within the team = bank of its table reads
     const uint32_t copy = q % kAppRepl;
@@ -128,14 +143,17 @@ __global__ __launch_bounds__(kThreads, 1) void append_crc_kernel(AppendArgs a) {
         uint64_t nload;  // pieces loaded: the payload's, then through the tail chunks (ct, ct + 16)
         uint32_t sh;     // source byte shift of every piece
         uint32_t t;      // piece index of the first tail chunk ct = P1 & ~15
+        uint32_t crc;    // (copy form)
         bool has_prev, has_next, nonempty;
     };
     uint64_t f0 = 0, f1 = 0, f2 = 0, f3 = 0;
+    uint32_t fc = 0;  // (copy form) the datagram's CRC from the CSR pass
     auto fetch = [&](uint32_t i) {
         f0 = a.off[i ? i - 1u : 0u];
         f1 = a.off[i];
         f2 = a.off[i + 1u];
         f3 = a.off[i + 2u <= n ? i + 2u : n];
+        if constexpr (!CRC) fc = a.crc[i];
     };
     auto make = [&](uint32_t i) -> Dg {
         Dg D;
@@ -150,6 +168,7 @@ __global__ __launch_bounds__(kThreads, 1) void append_crc_kernel(AppendArgs a) {
         D.sh = (uint32_t)((D.g.V0 - D.delta) & 3u);
         D.t = (uint32_t)(((D.g.P1 & ~(uint64_t)15) - D.g.V0) >> 4);
         D.nload = D.g.nv > (uint64_t)D.t + 2u ? D.g.nv : (uint64_t)D.t + 2u;
+        D.crc = fc;
         return D;
     };
     uint32_t d[kGroup][5];  // raw source dwords of the lane's pieces of one group
@@ -208,6 +227,7 @@ __global__ __launch_bounds__(kThreads, 1) void append_crc_kernel(AppendArgs a) {
                 uint32_t p[4] = {w[j][0], w[j][1], w[j][2], w[j][3]};
                 const uint64_t c = g.V0 + 16u * v;
                 if (c >= g.P0 && c + 16u <= g.P1) store16(c, p[0], p[1], p[2], p[3]);  // a payload chunk it owns
+                if constexpr (!CRC) continue;
                 const int32_t plo = (int32_t)((int64_t)g.P0 - (int64_t)c), phi = (int32_t)((int64_t)g.P1 - (int64_t)c);
                 if (plo > 0 || phi < 16) {  // first / last piece: only the payload's bytes count
 #pragma unroll
@@ -239,11 +259,14 @@ __global__ __launch_bounds__(kThreads, 1) void append_crc_kernel(AppendArgs a) {
         }
 
         // ---- team combine: each register shifted to the payload's end, XORed
-        uint32_t x = has ? nib(kAppM, 32u, (uint32_t)(D.g.nv - 1u - vlast), acc) : 0u;
+        uint32_t crc = D.crc;
+        if constexpr (CRC) {
+            uint32_t x = has ? nib(kAppM, 32u, (uint32_t)(D.g.nv - 1u - vlast), acc) : 0u;
 #pragma unroll
-        for (int k = 16; k >= 1; k >>= 1) x ^= (uint32_t)__shfl_xor((int)x, k, 64);
-        const uint32_t crc = D.nonempty ? ~nib(kAppTB + D.g.Z * 128u, 1u, 0u, x) : 0u;
-        if (a.crc && q == 0u) a.crc[i] = crc;
+            for (int k = 16; k >= 1; k >>= 1) x ^= (uint32_t)__shfl_xor((int)x, k, 64);
+            crc = D.nonempty ? ~nib(kAppTB + D.g.Z * 128u, 1u, 0u, x) : 0u;
+            if (a.crc && q == 0u) a.crc[i] = crc;
+        }
 
         // ---- the chunks holding the CRC, whole when the owner knows all 16 bytes
         // (by the lanes that hold their pieces)
@@ -280,12 +303,20 @@ __global__ __launch_bounds__(kThreads, 1) void append_crc_kernel(AppendArgs a) {
     }
 }
 
-#if LNL_APPEND_TWO_PASS
-// ---- experiments build: round 3's copy kernel after a CSR CRC pass -----------
+#if LNL_APPEND_MODE == 0
+// ---- the product: the copy kernel after the CSR CRC pass ------------------------
 // A team of 32 lanes per datagram writes its whole 16-byte destination chunks
-// from a dwordx4 + dword source load; the head chunk and the tail (payload
-// remainder + CRC) go one byte per lane.  Measured 340 us per config-3 call
-// after a 149 us CRC pass.
+// from a dwordx4 + dword source load (v_alignbyte to any byte shift); the
+// head chunk and the tail (payload remainder + CRC), which share chunks with
+// the neighbouring datagrams, go one byte per lane.  Each lane issues the
+// loads of up to kCopyU chunks before it stores any (round 3 issued one, then
+// stored it: one memory round trip per 512 bytes of a datagram).  20-odd
+// VGPRs, 8 waves per SIMD: the one-pass and team-copy kernels above hold more
+// state per lane and lose on occupancy.
+#ifndef LNL_APPEND_COPY_U
+#define LNL_APPEND_COPY_U 3  // chunk loads in flight per lane (1: round 3's kernel)
+#endif
+constexpr uint32_t kCopyU = LNL_APPEND_COPY_U;
 constexpr int kCopyThreads = 256;
 __device__ inline uint8_t out_byte(uint64_t x, uint64_t P1, uint64_t delta, uint32_t crc) {
     return x < P1 ? *LNL_G(const uint8_t, x - delta) : (uint8_t)(crc >> (8u * (uint32_t)(x - P1)));
@@ -296,9 +327,22 @@ __global__ __launch_bounds__(kCopyThreads) void append_copy_kernel(AppendArgs a)
     const uint32_t q = threadIdx.x % kAppTeam;
     const uint64_t o0 = a.off[0];
     const uint64_t dstb = (uint64_t)(uintptr_t)a.dst, srcb = (uint64_t)(uintptr_t)a.base - a.off0;
+    // the next datagram's offsets and CRC are fetched one datagram ahead
+    uint64_t ns = 0, ne = 0;
+    uint32_t ncrc = 0;
+    if (t < a.n) {
+        ns = a.off[t];
+        ne = a.off[t + 1];
+        ncrc = a.crc[t];
+    }
     for (uint32_t i = t; i < a.n; i += nt) {
-        const uint64_t s = a.off[i], e = a.off[i + 1];
-        const uint32_t crc = a.crc[i];
+        const uint64_t s = ns, e = ne;
+        const uint32_t crc = ncrc;
+        if (i + nt < a.n) {
+            ns = a.off[i + nt];
+            ne = a.off[i + nt + 1];
+            ncrc = a.crc[i + nt];
+        }
         const uint64_t P0 = dstb + (s - o0) + 4ull * i, P1 = P0 + (e - s), P2 = P1 + 4u;
         const uint64_t delta = P0 - (srcb + s);
         const uint64_t c0 = (P0 + 15u) & ~(uint64_t)15, c1 = P1 & ~(uint64_t)15;
@@ -306,23 +350,32 @@ __global__ __launch_bounds__(kCopyThreads) void append_copy_kernel(AppendArgs a)
             for (uint64_t x = P0 + q; x < P2; x += kAppTeam) *LNL_G(uint8_t, x) = out_byte(x, P1, delta, crc);
             continue;
         }
+        // the head chunk [P0, c0) and the tail [c1, P2), one byte per lane,
+        // loaded before the chunks so that their latency overlaps them
         const uint64_t x0 = P0 + q, x1 = c1 + q;
         const bool b0 = x0 < c0, b1 = x1 < P2;
         const uint8_t v0 = b0 ? out_byte(x0, P1, delta, crc) : 0;
         const uint8_t v1 = b1 ? out_byte(x1, P1, delta, crc) : 0;
-        const uint32_t c = (uint32_t)((c0 - delta) & 3u);
-        for (uint64_t w = c0 + 16ull * q; w < c1; w += 16ull * kAppTeam) {
-            const uint64_t sw = (w - delta) & ~(uint64_t)3;
-            const U4a v = *LNL_G(const U4a, sw);
-            uint4 o = make_uint4(v.x, v.y, v.z, v.w);
-            if (c) {
-                const uint32_t v4 = *LNL_G(const uint32_t, sw + 16);
-                o.x = __builtin_amdgcn_alignbyte(v.y, v.x, c);
-                o.y = __builtin_amdgcn_alignbyte(v.z, v.y, c);
-                o.z = __builtin_amdgcn_alignbyte(v.w, v.z, c);
-                o.w = __builtin_amdgcn_alignbyte(v4, v.w, c);
+        const uint32_t c = (uint32_t)((c0 - delta) & 3u);  // (the same for every chunk)
+        for (uint64_t wb = c0 + 16ull * q; wb < c1; wb += 16ull * kAppTeam * kCopyU) {
+            U4a v[kCopyU];
+            uint32_t v4[kCopyU];
+#pragma unroll
+            for (uint32_t u = 0; u < kCopyU; ++u) {
+                const uint64_t w = wb + 16ull * kAppTeam * u;
+                if (w < c1) {
+                    const uint64_t sw = (w - delta) & ~(uint64_t)3;
+                    v[u] = *LNL_G(const U4a, sw);
+                    v4[u] = c ? *LNL_G(const uint32_t, sw + 16) : 0u;  // (byte w - delta + 15: inside the payload)
+                }
             }
-            store16(w, o.x, o.y, o.z, o.w);
+#pragma unroll
+            for (uint32_t u = 0; u < kCopyU; ++u) {
+                const uint64_t w = wb + 16ull * kAppTeam * u;
+                if (w < c1)
+                    store16(w, __builtin_amdgcn_alignbyte(v[u].y, v[u].x, c), __builtin_amdgcn_alignbyte(v[u].z, v[u].y, c),
+                            __builtin_amdgcn_alignbyte(v[u].w, v[u].z, c), __builtin_amdgcn_alignbyte(v4[u], v[u].w, c));
+            }
         }
         if (b0) *LNL_G(uint8_t, x0) = v0;
         if (b1) *LNL_G(uint8_t, x1) = v1;
@@ -332,18 +385,28 @@ __global__ __launch_bounds__(kCopyThreads) void append_copy_kernel(AppendArgs a)
 
 }  // namespace
 
-bool append_two_pass() { return LNL_APPEND_TWO_PASS != 0; }
+bool append_two_pass() { return LNL_APPEND_MODE != 1; }
 
+#ifndef LNL_APPEND_WGS
+#define LNL_APPEND_WGS 16u  // copy kernel: workgroups per CU (teams stride over the datagrams)
+#endif
 hipError_t launch_append(const AppendArgs& a, int cus, hipStream_t stream) {
-#if LNL_APPEND_TWO_PASS
+#if LNL_APPEND_MODE == 0
     const uint32_t per = kCopyThreads / kAppTeam;
-    const uint32_t want = (a.n + per - 1) / per, cap = (uint32_t)cus * 16u;
+    const uint32_t want = (a.n + per - 1) / per, cap = (uint32_t)cus * LNL_APPEND_WGS;
     hipLaunchKernelGGL(append_copy_kernel, dim3(want < cap ? (want ? want : 1) : cap), dim3(kCopyThreads), 0, stream, a);
-#else
+#elif LNL_APPEND_MODE == 1
     // persistent: one workgroup per CU (LDS), teams striding over the datagrams
-    const uint32_t want = (a.n + kTeamsPerWg - 1) / kTeamsPerWg;
+    const uint32_t per = kThreads / kAppTeam;
+    const uint32_t want = (a.n + per - 1) / per;
     const uint32_t grid = want < (uint32_t)cus ? want : (uint32_t)cus;
-    hipLaunchKernelGGL(append_crc_kernel, dim3(grid ? grid : 1), dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL((append_team_kernel<true, kThreads>), dim3(grid ? grid : 1), dim3(kThreads), 0, stream, a);
+#else  // 2
+    // persistent: LNL_APPEND_COPY_WGS workgroups per CU, teams striding over the datagrams
+    const uint32_t per = kCopyTeamThreads / kAppTeam;
+    const uint32_t want = (a.n + per - 1) / per, cap = (uint32_t)cus * LNL_APPEND_COPY_WGS;
+    hipLaunchKernelGGL((append_team_kernel<false, kCopyTeamThreads>), dim3(want < cap ? (want ? want : 1) : cap),
+                       dim3(kCopyTeamThreads), 0, stream, a);
 #endif
     return hipGetLastError();
 }

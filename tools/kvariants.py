@@ -31,13 +31,18 @@ VARIANTS = {
     "run512p": "-DLNL_RUN_THREADS=512 -DLNL_RUN_PRIO=1",  # ... with progress-based issue priority
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
     "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
-    "app_2pass": "-DLNL_APPEND_TWO_PASS=1",          # outbound layer: round 3's CSR CRC pass + copy kernel
-    "app_r16": "-DLNL_APP_REPL=16",                 # one-pass append: lane tables in 16 copies (2-way bank sharing)
-    "app_r8": "-DLNL_APP_REPL=8",
-    "app_s16": "-DLNL_APP_SLICE16=1",               # one-pass append: slicing-by-16 piece CRC (16 independent lookups)
-    "app_g2": "-DLNL_APPEND_GROUP=2",               # one-pass append: pieces per lane loaded together (default 3)
+    "app_u1": "-DLNL_APPEND_COPY_U=1",              # outbound layer: round 3's copy kernel (one chunk load in flight per lane)
+    "app_u2": "-DLNL_APPEND_COPY_U=2",
+    "app_u4": "-DLNL_APPEND_COPY_U=4",
+    "app_team": "-DLNL_APPEND_MODE=2",              # outbound layer: CSR CRC pass + the team copy (ownership rule)
+    "app_1pass": "-DLNL_APPEND_MODE=1",             # outbound layer in one pass (the team computes the CRCs)
+    "app_1pass_r16": "-DLNL_APPEND_MODE=1 -DLNL_APP_REPL=16",   # ... lane tables in 16 copies
+    "app_1pass_s16": "-DLNL_APPEND_MODE=1 -DLNL_APP_SLICE16=1",  # ... slicing-by-16 piece CRC
+    "app_1pass_t512": "-DLNL_APPEND_MODE=1 -DLNL_APPEND_THREADS=512",  # ... 512-thread workgroups (8 waves per CU)
+    "app_g2": "-DLNL_APPEND_GROUP=2",               # team kernels: pieces per lane loaded together (default 3)
     "app_g4": "-DLNL_APPEND_GROUP=4",
-    "app_t512": "-DLNL_APPEND_THREADS=512",         # one-pass append: 512-thread workgroups (8 waves per CU)
+    "app_w8": "-DLNL_APPEND_WGS=8u",                # copy kernel: workgroups per CU (default 16)
+    "app_w32": "-DLNL_APPEND_WGS=32u",
     "prep8k": "-DLNL_SPAN_PREP_BLOCKS=8192u",       # span pre-pass: 8192 workgroups (before: 1 % slower than 1024)
     "prep256": "-DLNL_SPAN_PREP_BLOCKS=256u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
