@@ -66,6 +66,12 @@ constexpr uint32_t kWin1 = 12;    // window chunks (64 offsets each) loaded ahea
 #ifndef LNL_SPAN_PRIO
 #define LNL_SPAN_PRIO 0  // 0: progress-based issue priority; 1: static (experiment); 2: none
 #endif
+#ifndef LNL_SPAN_ROWS_LATE
+#define LNL_SPAN_ROWS_LATE 0  // 1: a wave-batch's first two rows go out with its offset window, not with its probe
+#endif
+#ifndef LNL_SPAN_FIN_LDS
+#define LNL_SPAN_FIN_LDS 0  // 1: the heads' final map from the LDS tables (TB, TA), not the global FIN table
+#endif
 constexpr uint32_t kTabBytes = kSpanTabLds * 4;
 // LDS (bytes): the fold tables (crc32c_span.h) first -- the Horner's byte
 // lookups then address them with a 16-bit immediate offset -- and a zero
@@ -420,7 +426,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             const uint32_t i = threadIdx.x + j * kThreads;
             row_load(tv[j], (uint64_t)(uintptr_t)A.tab + 16u * (i < kTabPieces ? i : 0u));
         }
-        if (has0) {
+        if (has0 && !LNL_SPAN_ROWS_LATE) {
             issue(0u, ra);
             issue(1u, rb);  // R >= 16
             asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -449,9 +455,13 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         if (wb != gw) {  // a later wave-batch (batches larger than one round): the same start
             set_wb(wb);
             probe();
+#if LNL_SPAN_ROWS_LATE
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
             issue(0u, ra);
             issue(1u, rb);
             asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+#endif
         }
         // ---- this lane's datagrams ----------------------------------------
         // [k0, k1): the datagrams ending in this segment; k0 = #{m >= 1 :
@@ -504,8 +514,16 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint32_t mm = a + 64u * c + lane;
                 off_load(wv[c], (uint64_t)(uintptr_t)(A.off + (mm < n ? mm : n)));
             }
+#if LNL_SPAN_ROWS_LATE
+            // the first two rows go out behind the window: one counted wait
+            // for the window, the rows stream on
+            issue(0u, ra);
+            issue(1u, rb);
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+#else
             // the window (behind the first rows, which land first)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 #pragma unroll
             for (int c = 0; c < (int)kWin1; ++c) {
                 asm volatile("" : "+v"(wv[c]));
@@ -1067,7 +1085,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             const uint32_t thdr_prev = (uint32_t)__shfl((int)thdr, src, 64);
             if (htrack && lane != 0u && hk < n) {
                 const uint32_t m = hinfo & 0xFFu, e = (hinfo >> 8) & 0xFFu;
+#if LNL_SPAN_FIN_LDS
+                const uint32_t crc = final_crc_lds(tab_base, e, lnl_span_rows(A.tab, m, tprev) ^ r_head);
+#else
                 const uint32_t crc = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tprev) ^ r_head);
+#endif
                 // (the head's length: its part in the previous segment and in this one)
                 store_result(A, hk, crc, (Sb - tcs_prev) + (m << 7) - e, thdr_prev);
             }
@@ -1116,7 +1138,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     const uint32_t tinf = lane == 63u ? (tcs | (thdr << 16)) : get_x(kSpanXchTailInfo);
                     if ((info & kSpanHeadBit) && hidx < n) {
                         const uint32_t m = info & 0xFFu, e = (info >> 8) & 0xFFu;
+#if LNL_SPAN_FIN_LDS
+                        const uint32_t crc = final_crc_lds(tab_base, e, lnl_span_rows(A.tab, m, tail) ^ head);
+#else
                         const uint32_t crc = lnl_span_final(A.tab, e, lnl_span_rows(A.tab, m, tail) ^ head);
+#endif
                         store_result(A, hidx, crc, (Sb - (tinf & 0xFFFFu)) + (m << 7) - e, tinf >> 16);
                     }
                 }

@@ -24,6 +24,10 @@ VARIANTS = {
     "span_nofold": "-DLNL_SPAN_DIAG=1",             # CSR span kernel without its folds (wrong CRCs)
     "span_noev": "-DLNL_SPAN_DIAG=2",               # CSR span kernel: rows + network only (wrong CRCs)
     "span_prev": ("", None, "build/span_prev.hip"),  # A/B: the span kernel source saved in build/ (untracked)
+    "span_late": "-DLNL_SPAN_ROWS_LATE=1",          # span kernel: first rows issued with the offset window, not the probe
+    "span_finlds": "-DLNL_SPAN_FIN_LDS=1",          # span kernel: heads' final map from the LDS tables
+    "span_late_fin": "-DLNL_SPAN_ROWS_LATE=1 -DLNL_SPAN_FIN_LDS=1",
+    "span_late_tl": "-DLNL_SPAN_ROWS_LATE=1 -DLNL_SPAN_DIAG=16",
     "span_noprio": "-DLNL_SPAN_PRIO=2",            # span kernel: no issue-priority balancing
     "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
     "span_timeline": "-DLNL_SPAN_DIAG=16",          # span kernel: per-wave timeline into out[] (wrong CRCs)
