@@ -376,6 +376,9 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
     hipError_t e = lnl::launch_span(g, S.cus, st);
     if (e != hipSuccess) return hip_fail(e, "span kernel launch");
     ++sc->calls;
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 32)
+    return 0;  // diagnostic build only: no batch kernel (overflow datagrams left unwritten)
+#endif
     lnl::BatchArgs o = a;
     o.perm = g.ovf;
     o.perm_n = g.ctl + 1;

@@ -66,8 +66,16 @@ constexpr uint32_t kWin1 = 12;    // window chunks (64 offsets each) loaded ahea
 #ifndef LNL_SPAN_PRIO
 #define LNL_SPAN_PRIO 0  // 0: progress-based issue priority; 1: static (experiment); 2: none
 #endif
+// Round 4 (tools/kvariants.py, config-3 CSR call, one box: 153.8 -> 151.1 us,
+// filter 146.6 -> 144.7 us): a wave-batch's first two rows go out behind its
+// offset window rather than with its probe, so the probe and the window are not
+// queued behind 16 MB of rows (0: round 3's order); a partial flush (the
+// segment's end) looks up tables in the lanes that fold only (0: all lanes).
 #ifndef LNL_SPAN_ROWS_LATE
-#define LNL_SPAN_ROWS_LATE 0  // 1: a wave-batch's first two rows go out with its offset window, not with its probe
+#define LNL_SPAN_ROWS_LATE 1
+#endif
+#ifndef LNL_SPAN_FOLD_MASK
+#define LNL_SPAN_FOLD_MASK 1
 #endif
 #ifndef LNL_SPAN_FIN_LDS
 #define LNL_SPAN_FIN_LDS 0  // 1: the heads' final map from the LDS tables (TB, TA), not the global FIN table
@@ -782,11 +790,21 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             Pieces<0>::write(ea, live_state, kZero32);
 #if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 1)
             const uint32_t r = v[0] ^ v[31];  // diagnostic build only: no fold (wrong CRCs)
+#elif LNL_SPAN_FOLD_MASK
+            // only the lanes that fold look up tables: a partial flush (the
+            // segment's end) costs LDS in proportion to its entries
+            uint32_t r = 0u;
+            if (act) r = phi_lds(T, tab_base, v);
 #else
             const uint32_t r = phi_lds(T, tab_base, v);
 #endif
             const uint32_t type = (mt.y >> 8) & 3u, e = mt.y & 127u;  // mt.y: e | type << 8 | hdr << 10 | len << 18
+#if LNL_SPAN_FOLD_MASK
+            uint32_t crc = 0u;
+            if (act) crc = final_crc_lds(tab_base, e, r);
+#else
             const uint32_t crc = final_crc_lds(tab_base, e, r);
+#endif
             if (act && type == kTypeNormal && mt.x < n) {  // (the index check only guards the store)
                 store_result(A, mt.x, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
             }

@@ -24,13 +24,15 @@ VARIANTS = {
     "span_nofold": "-DLNL_SPAN_DIAG=1",             # CSR span kernel without its folds (wrong CRCs)
     "span_noev": "-DLNL_SPAN_DIAG=2",               # CSR span kernel: rows + network only (wrong CRCs)
     "span_prev": ("", None, "build/span_prev.hip"),  # A/B: the span kernel source saved in build/ (untracked)
-    "span_late": "-DLNL_SPAN_ROWS_LATE=1",          # span kernel: first rows issued with the offset window, not the probe
+    "span_r3": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0",  # span kernel as in round 3 (first rows with the probe; full-wave partial flushes)
+    "span_early": "-DLNL_SPAN_ROWS_LATE=0",         # span kernel: first rows issued with the probe (round 3)
+    "span_nofmask": "-DLNL_SPAN_FOLD_MASK=0",       # span kernel: partial flushes look up tables in every lane (round 3)
     "span_finlds": "-DLNL_SPAN_FIN_LDS=1",          # span kernel: heads' final map from the LDS tables
-    "span_late_fin": "-DLNL_SPAN_ROWS_LATE=1 -DLNL_SPAN_FIN_LDS=1",
-    "span_late_tl": "-DLNL_SPAN_ROWS_LATE=1 -DLNL_SPAN_DIAG=16",
+    "span_nob": "-DLNL_SPAN_DIAG=32",               # span kernel, no batch kernel after it (overflow datagrams unwritten)
     "span_noprio": "-DLNL_SPAN_PRIO=2",            # span kernel: no issue-priority balancing
     "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
     "span_timeline": "-DLNL_SPAN_DIAG=16",          # span kernel: per-wave timeline into out[] (wrong CRCs)
+    "span_r3_tl": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0 -DLNL_SPAN_DIAG=16",
     "run512": "-DLNL_RUN_THREADS=512",              # lane-run kernel: one 512-thread workgroup per CU
     "run512p": "-DLNL_RUN_THREADS=512 -DLNL_RUN_PRIO=1",  # ... with progress-based issue priority
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
