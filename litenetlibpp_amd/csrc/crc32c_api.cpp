@@ -428,7 +428,10 @@ uint32_t run_plan(size_t stride, uint32_t len, uint32_t n, lnl::RunArgs& r) {
     const uint32_t low = S & (0u - S);  // largest power of two dividing S
     const uint32_t p = low >= 128u ? 1u : 128u / low;
     const uint32_t k = LNL_RUN_K;
-    const uint32_t q = p > k ? p : k;
+    uint32_t q = p > k ? p : k;
+#ifdef LNL_RUN_QMIN  // experiments: lanes at least QMIN datagrams apart (a multiple of q)
+    while (q < (uint32_t)LNL_RUN_QMIN) q *= 2u;
+#endif
     if ((uint64_t)64u * q * S >= (1ull << 31)) return 0;  // per-lane 32-bit offsets
     const uint32_t super = 64u * q;
     const uint32_t n_main = n - n % super;

@@ -33,6 +33,8 @@ VARIANTS = {
     "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
     "span_timeline": "-DLNL_SPAN_DIAG=16",          # span kernel: per-wave timeline into out[] (wrong CRCs)
     "span_r3_tl": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0 -DLNL_SPAN_DIAG=16",
+    "run3": "-DLNL_RUN_VROWS=1",                    # lane-run kernel: three rows in flight per wave (one LDS-DMA, two VGPR)
+    "run3_nt0": "-DLNL_RUN_VROWS=1 -DLNL_RUN_AUX=0",
     "run512": "-DLNL_RUN_THREADS=512",              # lane-run kernel: one 512-thread workgroup per CU
     "run512p": "-DLNL_RUN_THREADS=512 -DLNL_RUN_PRIO=1",  # ... with progress-based issue priority
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
@@ -81,6 +83,9 @@ VARIANTS = {
     "batch": "-DLNL_NO_RUN",                        # any-layout batch kernel for everything
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
     "k16": "-DLNL_RUN_K=16",
+    "q32": "-DLNL_RUN_QMIN=32",                     # lane runs 32 datagrams apart (default: 16 at S = 1400)
+    "q64": "-DLNL_RUN_QMIN=64",
+    "k4q32": "-DLNL_RUN_K=4 -DLNL_RUN_QMIN=32",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
     "run_late": "-DLNL_RUN_EARLY_ROWS=0",           # run kernel: first rows issued after the tables land (before round 3)
     # (round 1's uniform / segment / pair CSR paths: tools/experiments/csr_experiment_kernels.patch)
