@@ -4,7 +4,12 @@
 // wire form net_manager::send_raw puts on the socket with the layer on
 // (/root/reference/src/lnl/net_manager.cpp:515-521).
 //
-// One pass over the payload (crc32c_append.h has the algebra and the
+// The product (LNL_APPEND_MODE 0): the CSR CRC pass (crc32c_span.hip) into
+// crc[], then append_copy_kernel below -- 32 lanes per datagram, whole 16-byte
+// destination chunks, up to three chunk loads in flight per lane.
+//
+// Experiments build only (tools/kvariants.py app_1pass*, app_team): the layer
+// in ONE pass over the payload (crc32c_append.h has the algebra and the
 // ownership rule).  A team of 32 lanes takes one datagram; lane q loads the
 // 16 source bytes of destination chunks V0 + 16 v, v = q, q + 32, ... (a
 // dwordx4 + dword at any byte shift, aligned with v_alignbyte), stores the
@@ -16,11 +21,10 @@
 // together, and writes the chunks that hold the CRC -- whole 16-byte stores,
 // the next datagram's first bytes included, whenever it knows all 16 -- and,
 // only where a chunk is shared with a datagram of < 12 bytes or lies at the
-// burst's edges, single bytes.
-//
-// One 1024-thread workgroup per CU (the tables take 104 KiB of LDS), teams
-// striding over the datagrams so that the whole grid writes one front of the
-// burst.
+// burst's edges, single bytes.  One 1024-thread workgroup per CU (the tables
+// take 104 KiB of LDS).  Parity-green, and 752-845 us per config-3 call
+// against the two passes' 467: its per-datagram work runs on all 32 lanes
+// at 4 waves per SIMD.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
