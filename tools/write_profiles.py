@@ -24,7 +24,7 @@ from prof_summary import from_db, short  # noqa: E402
 PRODUCT_KERNELS = ("crc32c_", "bucket_count", "bucket_scatter", "bucket_hist", "bucket_scan", "bucket_place",
                    "pair_count", "pair_scatter", "seg_prep", "seg_fixup", "verify_from_wire", "csr_plan",
                    "dispatch_", "xor_layer", "xor_flat", "xor_csr_flat", "xor_csr_stream", "xor_csr_grid",
-                   "xor_chunk_map", "span_prep", "append_kernel")
+                   "xor_chunk_map", "span_prep", "append_")
 
 
 def main():
