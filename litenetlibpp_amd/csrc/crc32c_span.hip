@@ -77,6 +77,9 @@ constexpr uint32_t kWin1 = 12;    // window chunks (64 offsets each) loaded ahea
 #ifndef LNL_SPAN_FOLD_MASK
 #define LNL_SPAN_FOLD_MASK 1
 #endif
+#ifndef LNL_SPAN_F_MASK
+#define LNL_SPAN_F_MASK 0  // 1: F(b) read by the lanes with a boundary only (experiment)
+#endif
 #ifndef LNL_SPAN_FIN_LDS
 #define LNL_SPAN_FIN_LDS 0  // 1: the heads' final map from the LDS tables (TB, TA), not the global FIN table
 #endif
@@ -128,7 +131,9 @@ __device__ LNL_INLINE void append(uint32_t* cnt, uint32_t* list, bool take, uint
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
     base = (uint32_t)__shfl((int)base, (int)leader, 64);
-    if (take) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = value;
+    // rank among the taking lanes (mbcnt: no 64-bit lane mask held in registers)
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (take) list[base + rank] = value;
 }
 
 __device__ LNL_INLINE uint32_t clamp16(int64_t v) { return v <= 0 ? 0u : (v >= 0xFFFF ? 0xFFFFu : (uint32_t)v); }
@@ -410,8 +415,12 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
     uint32_t pidx = 0;
     uint64_t pv = 0;
     auto probe = [&]() {
-        const double f = (double)(line0 - G.S0) / (double)G.Pn;
-        const int64_t pi = (int64_t)(f * (double)n) - 32 * 64 + (int64_t)lane * 64;
+        // (fp32: only the probe's centre; a miss costs a 64-ary search, and the
+        // error, ~1e-7 n, is far inside the probe's +-2,048 entries)
+        const float f = (float)(line0 - G.S0) / (float)G.Pn;
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));  // (not a 64-bit per-lane constant held across the loop)
+        const int64_t pi = (int64_t)(f * (float)n) + (int64_t)((int32_t)(ln * 64u) - 32 * 64);
         pidx = pi < 0 ? 0u : (pi > (int64_t)n ? n : (uint32_t)pi);
         off_load(pv, (uint64_t)(uintptr_t)(A.off + pidx));
     };
@@ -882,7 +891,13 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 uint32_t ad[8];
 #pragma unroll
                 for (int p = 0; p < 8; ++p) ad[p] = (uint32_t)p < bp ? zero_addr : r0 ^ (16u * p);
+#if LNL_SPAN_F_MASK
+                // only the lanes with a boundary read F: a row's other lanes
+                // would move 128 bytes each through the LDS for nothing
+                if (ev) read_row<0>(ad, F);
+#else
                 read_row<0>(ad, F);
+#endif
             }
             const bool head = cs < 0;
             // (a normal datagram started in this segment: len < Sb < 2^14)
@@ -1145,10 +1160,16 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     put_x(kSpanXchTailInfo, tcs | (thdr << 16));
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the parts are out before the arrival
+                // (the epoch through an empty asm here: left alone, the compiler
+                // hoists both arrival values out of the wave-batch loop and
+                // spills them across the rows)
+                uint64_t ep = A.epoch;
+                uint32_t sd = side;
+                asm volatile("" : "+s"(ep), "+v"(sd));
                 const uint64_t prior = __hip_atomic_exchange(reinterpret_cast<uint64_t*>(xb + kSpanXchFlag),
-                                                             span_arrival(A.epoch, side), __ATOMIC_RELAXED,
+                                                             span_arrival(ep, sd), __ATOMIC_RELAXED,
                                                              __HIP_MEMORY_SCOPE_AGENT);
-                if (prior == span_arrival(A.epoch, kSpanSideHead ^ kSpanSideTail ^ side)) {
+                if (prior == span_arrival(ep, kSpanSideHead ^ kSpanSideTail ^ sd)) {
                     const uint32_t head = lane == 0u ? r_head : get_x(kSpanXchHead);
                     const uint32_t hidx = lane == 0u ? hk : get_x(kSpanXchHeadIdx);
                     const uint32_t info = lane == 0u ? (hinfo | (htrack ? kSpanHeadBit : 0u)) : get_x(kSpanXchHeadInfo);

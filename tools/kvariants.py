@@ -27,6 +27,8 @@ VARIANTS = {
     "span_r3": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0",  # span kernel as in round 3 (first rows with the probe; full-wave partial flushes)
     "span_early": "-DLNL_SPAN_ROWS_LATE=0",         # span kernel: first rows issued with the probe (round 3)
     "span_nofmask": "-DLNL_SPAN_FOLD_MASK=0",       # span kernel: partial flushes look up tables in every lane (round 3)
+    "span_ffmask": "-DLNL_SPAN_F_MASK=1",           # span kernel: F(b) read by the boundary lanes only
+    "span_ffmask_tl": "-DLNL_SPAN_F_MASK=1 -DLNL_SPAN_DIAG=16",
     "span_finlds": "-DLNL_SPAN_FIN_LDS=1",          # span kernel: heads' final map from the LDS tables
     "span_nob": "-DLNL_SPAN_DIAG=32",               # span kernel, no batch kernel after it (overflow datagrams unwritten)
     "span_noprio": "-DLNL_SPAN_PRIO=2",            # span kernel: no issue-priority balancing
