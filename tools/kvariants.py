@@ -27,6 +27,9 @@ VARIANTS = {
     "span_r3": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0",  # span kernel as in round 3 (first rows with the probe; full-wave partial flushes)
     "span_early": "-DLNL_SPAN_ROWS_LATE=0",         # span kernel: first rows issued with the probe (round 3)
     "span_nofmask": "-DLNL_SPAN_FOLD_MASK=0",       # span kernel: partial flushes look up tables in every lane (round 3)
+    "span_ef0": "-DLNL_SPAN_EARLY_FLUSH=0",         # fused walk kernel: no early flush (before round 4)
+    "span_ef44": "-DLNL_SPAN_EARLY_FLUSH=44",       # ... fold a stash of >= N entries at a row step's start (product: 50)
+    "span_ef56": "-DLNL_SPAN_EARLY_FLUSH=56",
     "span_ffmask": "-DLNL_SPAN_F_MASK=1",           # span kernel: F(b) read by the boundary lanes only
     "span_ffmask_tl": "-DLNL_SPAN_F_MASK=1 -DLNL_SPAN_DIAG=16",
     "span_finlds": "-DLNL_SPAN_FIN_LDS=1",          # span kernel: heads' final map from the LDS tables
