@@ -275,7 +275,8 @@ struct ScratchCache {
     uint64_t tick = 0;
 
     // the entry for st, at least `words` long (the first zero_words zeroed
-    // whenever it is (re)allocated; *fresh says so); evicts beyond the bound
+    // whenever it is (re)allocated, and its call count restarted); evicts
+    // beyond the bound
     int get(hipStream_t st, size_t words, size_t zero_words, SpanScratch** out) {
         const StreamKey key = stream_key(st);
         SpanScratch& s = m[key];
