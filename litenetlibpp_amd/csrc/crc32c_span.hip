@@ -80,6 +80,14 @@ constexpr uint32_t kWin1 = 12;    // window chunks (64 offsets each) loaded ahea
 #ifndef LNL_SPAN_EARLY_FLUSH
 #define LNL_SPAN_EARLY_FLUSH 50  // WALK kernel: fold a stash holding this many entries at a row step's start (0: off)
 #endif
+// The segment's end (round 4): its tail is folded in registers rather than
+// through the stash (1), and the last partial flush in the same pass (2, the
+// default; 0: round 3's stash path).  Config-3 call 150.3 -> 148.3 us, filter
+// 147.9 -> 143.8, fused walk 337.4 -> 335.4 (tools/kvariants.py, one box);
+// the end phase 6.2 -> 4.6 us in the per-wave timeline.
+#ifndef LNL_SPAN_TAIL_REG
+#define LNL_SPAN_TAIL_REG 2
+#endif
 #ifndef LNL_SPAN_F_MASK
 #define LNL_SPAN_F_MASK 0  // 1: F(b) read by the lanes with a boundary only (experiment)
 #endif
@@ -1099,6 +1107,63 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // segment is an overflow datagram: its tail is folded but not used --
         // the next segment has no head -- and the batch kernel writes its CRC.
         // So no boundary past the segment is needed here.) --------------------
+#if LNL_SPAN_TAIL_REG
+        // (the tail folded in registers, after what the stash still holds:
+        // no stash round trip and no second flush for it)
+        {
+            const bool tail = is_open() && k < n && cs >= 0 && cs < (int32_t)Sb;
+#if LNL_SPAN_TAIL_REG == 2
+            // full flushes first; the last partial one folds in the same pass as
+            // the tails (the row registers are free now: no parking)
+            while (st_tail - st_head >= kFlush) flush(kFlush, sA);
+            const uint32_t nf = st_tail - st_head;
+            if (nf != 0u) {
+                const bool act = lane < nf;
+                uint32_t slot = head_slot + lane;
+                slot = slot >= kCap ? slot - kCap : slot;
+                const uint32_t ea = stash + (act ? slot : 0u) * kEntry;
+                uint32_t v[32];
+                ds_read8(ea, v);
+                uint2 mt;
+                asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(mt) : "v"(meta + (act ? slot : 0u) * 8u) : "memory");
+                uint32_t r = 0u, rt = 0u;
+                if (act) r = phi_lds(T, tab_base, v);
+                if (tail) rt = phi_lds(T, tab_base, sA);
+                const uint32_t type = (mt.y >> 8) & 3u, e = mt.y & 127u;
+                uint32_t crc = 0u;
+                if (act) crc = final_crc_lds(tab_base, e, r);
+                if (act && type == kTypeNormal && mt.x < n) store_result(A, mt.x, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
+                const uint32_t hs = hpos - st_head;
+                const uint32_t rh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (hs & 63u)), (int)r);
+                if (hpend && hs < nf) {
+                    r_head = rh;
+                    hpend = false;
+                }
+                st_head += nf;
+                head_slot += nf;
+                head_slot = head_slot >= kCap ? head_slot - kCap : head_slot;
+                if (tail) r_tail = rt;
+            } else if (tail) {
+                r_tail = phi_lds(T, tab_base, sA);
+            }
+            if (tail) {
+                tcs = (uint32_t)cs;
+                thdr = chdr;
+            }
+#else
+            for (;;) {
+                const uint32_t cnt = st_tail - st_head;
+                if (cnt == 0u) break;
+                flush(cnt < kFlush ? cnt : kFlush, sA);
+            }
+            if (tail) {
+                r_tail = phi_lds(T, tab_base, sA);
+                tcs = (uint32_t)cs;
+                thdr = chdr;
+            }
+#endif
+        }
+#else
         {
             const bool tail = is_open() && k < n && cs >= 0 && cs < (int32_t)Sb;
             bool tdone = !tail;
@@ -1121,6 +1186,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 tdone = true;
             }
         }
+#endif
         LNL_TL(4);
         // heads: CRC = ~step^(-8e)(step^(1024 m) tail ^ head), the tail from
         // the previous lane; lane 0's from the previous wave-batch (below)

@@ -24,12 +24,14 @@ VARIANTS = {
     "span_nofold": "-DLNL_SPAN_DIAG=1",             # CSR span kernel without its folds (wrong CRCs)
     "span_noev": "-DLNL_SPAN_DIAG=2",               # CSR span kernel: rows + network only (wrong CRCs)
     "span_prev": ("", None, "build/span_prev.hip"),  # A/B: the span kernel source saved in build/ (untracked)
-    "span_r3": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0",  # span kernel as in round 3 (first rows with the probe; full-wave partial flushes)
+    "span_r3": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0 -DLNL_SPAN_TAIL_REG=0",  # span kernel as in round 3 (first rows with the probe; full-wave partial flushes)
     "span_early": "-DLNL_SPAN_ROWS_LATE=0",         # span kernel: first rows issued with the probe (round 3)
     "span_nofmask": "-DLNL_SPAN_FOLD_MASK=0",       # span kernel: partial flushes look up tables in every lane (round 3)
     "span_ef0": "-DLNL_SPAN_EARLY_FLUSH=0",         # fused walk kernel: no early flush (before round 4)
     "span_ef44": "-DLNL_SPAN_EARLY_FLUSH=44",       # ... fold a stash of >= N entries at a row step's start (product: 50)
     "span_ef56": "-DLNL_SPAN_EARLY_FLUSH=56",
+    "span_tstash": "-DLNL_SPAN_TAIL_REG=0",         # span kernel: the segment's tail through the stash (round 3)
+    "span_treg1": "-DLNL_SPAN_TAIL_REG=1",          # ... folded in registers after a separate last flush (product: 2)
     "span_ffmask": "-DLNL_SPAN_F_MASK=1",           # span kernel: F(b) read by the boundary lanes only
     "span_ffmask_tl": "-DLNL_SPAN_F_MASK=1 -DLNL_SPAN_DIAG=16",
     "span_finlds": "-DLNL_SPAN_FIN_LDS=1",          # span kernel: heads' final map from the LDS tables
@@ -37,7 +39,7 @@ VARIANTS = {
     "span_noprio": "-DLNL_SPAN_PRIO=2",            # span kernel: no issue-priority balancing
     "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
     "span_timeline": "-DLNL_SPAN_DIAG=16",          # span kernel: per-wave timeline into out[] (wrong CRCs)
-    "span_r3_tl": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0 -DLNL_SPAN_DIAG=16",
+    "span_r3_tl": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0 -DLNL_SPAN_TAIL_REG=0 -DLNL_SPAN_DIAG=16",
     "run3": "-DLNL_RUN_VROWS=1",                    # lane-run kernel: three rows in flight per wave (one LDS-DMA, two VGPR)
     "run3_nt0": "-DLNL_RUN_VROWS=1 -DLNL_RUN_AUX=0",
     "run512": "-DLNL_RUN_THREADS=512",              # lane-run kernel: one 512-thread workgroup per CU
