@@ -321,6 +321,10 @@ __global__ __launch_bounds__(THREADS, CRC ? 1 : 2) void append_team_kernel(Appen
 #define LNL_APPEND_COPY_U 3  // chunk loads in flight per lane (1: round 3's kernel)
 #endif
 constexpr uint32_t kCopyU = LNL_APPEND_COPY_U;
+#ifndef LNL_APPEND_COPY_DPP
+#define LNL_APPEND_COPY_DPP 0  // 1: aligned source chunks, the next lane's by DPP (experiment: parity-green,
+                               // 499 vs 466 us per config-3 call -- the unaligned loads are not what bounds the copy)
+#endif
 constexpr int kCopyThreads = 256;
 __device__ inline uint8_t out_byte(uint64_t x, uint64_t P1, uint64_t delta, uint32_t crc) {
     return x < P1 ? *LNL_G(const uint8_t, x - delta) : (uint8_t)(crc >> (8u * (uint32_t)(x - P1)));
@@ -360,6 +364,60 @@ __global__ __launch_bounds__(kCopyThreads) void append_copy_kernel(AppendArgs a)
         const bool b0 = x0 < c0, b1 = x1 < P2;
         const uint8_t v0 = b0 ? out_byte(x0, P1, delta, crc) : 0;
         const uint8_t v1 = b1 ? out_byte(x1, P1, delta, crc) : 0;
+#if LNL_APPEND_COPY_DPP
+        // Experiment: every lane loads the 16-byte ALIGNED source chunk under its
+        // destination chunk; the bytes past it are the next lane's chunk,
+        // taken with a DPP wave shift (the team's last lane loads its own), so
+        // each chunk is one aligned dwordx4 instead of an unaligned dwordx4 +
+        // dword.  Lanes past the payload's end still load (their chunk holds
+        // payload bytes its left neighbour needs) when it starts inside it.
+        {
+            const uint32_t off = (uint32_t)((c0 - delta) & 15u), kd = off >> 2, cb = off & 3u;
+            const uint64_t send = srcb + e;  // one past the payload's last source byte
+            for (uint64_t wb = c0 + 16ull * q; wb - 16ull * q < c1; wb += 16ull * kAppTeam * kCopyU) {
+                uint32_t d[kCopyU][8];
+#pragma unroll
+                for (uint32_t u = 0; u < kCopyU; ++u) {
+                    const uint64_t w = wb + 16ull * kAppTeam * u;
+                    const uint64_t sa = (w - delta) & ~(uint64_t)15;
+                    U4a va{0u, 0u, 0u, 0u};
+                    if (sa < send) va = *LNL_G(const U4a, sa);
+                    d[u][0] = va.x;
+                    d[u][1] = va.y;
+                    d[u][2] = va.z;
+                    d[u][3] = va.w;
+                    d[u][4] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)va.x, 0x130, 0xf, 0xf, false);  // wave_shl:1
+                    d[u][5] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)va.y, 0x130, 0xf, 0xf, false);
+                    d[u][6] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)va.z, 0x130, 0xf, 0xf, false);
+                    d[u][7] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)va.w, 0x130, 0xf, 0xf, false);
+                    if (q == kAppTeam - 1u && w < c1 && off != 0u) {  // the team's last lane: its own next chunk
+                        const U4a vb = *LNL_G(const U4a, sa + 16u);
+                        d[u][4] = vb.x;
+                        d[u][5] = vb.y;
+                        d[u][6] = vb.z;
+                        d[u][7] = vb.w;
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kCopyU; ++u) {
+                    const uint64_t w = wb + 16ull * kAppTeam * u;
+                    if (w < c1) {
+                        uint32_t m[5];
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) {
+                            const uint32_t a0 = d[u][j], a1 = d[u][j + 1], a2 = d[u][j + 2], a3 = d[u][(j + 3) & 7];
+                            m[j] = kd == 0u ? a0 : (kd == 1u ? a1 : (kd == 2u ? a2 : a3));
+                        }
+                        store16(w, __builtin_amdgcn_alignbyte(m[1], m[0], cb), __builtin_amdgcn_alignbyte(m[2], m[1], cb),
+                                __builtin_amdgcn_alignbyte(m[3], m[2], cb), __builtin_amdgcn_alignbyte(m[4], m[3], cb));
+                    }
+                }
+            }
+        }
+        if (b0) *LNL_G(uint8_t, x0) = v0;
+        if (b1) *LNL_G(uint8_t, x1) = v1;
+        continue;
+#endif
         const uint32_t c = (uint32_t)((c0 - delta) & 3u);  // (the same for every chunk)
         for (uint64_t wb = c0 + 16ull * q; wb < c1; wb += 16ull * kAppTeam * kCopyU) {
             U4a v[kCopyU];

@@ -46,6 +46,7 @@ VARIANTS = {
     "run512p": "-DLNL_RUN_THREADS=512 -DLNL_RUN_PRIO=1",  # ... with progress-based issue priority
     "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
     "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
+    "app_dpp": "-DLNL_APPEND_COPY_DPP=1",           # outbound copy: aligned source chunks, neighbour's by DPP
     "app_u1": "-DLNL_APPEND_COPY_U=1",              # outbound layer: round 3's copy kernel (one chunk load in flight per lane)
     "app_u2": "-DLNL_APPEND_COPY_U=2",
     "app_u4": "-DLNL_APPEND_COPY_U=4",
