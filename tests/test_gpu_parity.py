@@ -259,6 +259,27 @@ def test_csr_span_dense_small_datagrams(P):
     assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
 
 
+@pytest.mark.parametrize("order", ["small_first", "large_first"])
+def test_csr_span_skewed_density(P, order):
+    """A batch whose datagram density changes half way (tiny datagrams, then
+    MTU-sized ones, or the reverse): an index interpolated from a byte position
+    misses by hundreds of thousands of datagrams, so the setup's windows are
+    found by the fallback searches (probe, 64-ary search), not the first guess."""
+    rng = np.random.default_rng(["small_first", "large_first"].index(order) + 410)
+    n_small, n_large = 700_000, 500_000
+    small = rng.integers(0, 40, n_small)
+    large = rng.integers(1000, 1433, n_large)
+    lens = np.concatenate([small, large] if order == "small_first" else [large, small])
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(17)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(411)
+    d = torch.randint(0, 256, (int(off[-1]) + 5,), dtype=torch.uint8, device="cuda", generator=g)
+    got = u32(P.batch_csr(d, dev(off.view(np.int64), torch.int64)))
+    exp = oracle.batch_csr(d.cpu().numpy(), off)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{order}: {bad.size} mismatches, first at {bad[:5]}"
+
+
 def test_verify_mode_bucketed(P):
     rng = np.random.default_rng(22)
     n = 30000
