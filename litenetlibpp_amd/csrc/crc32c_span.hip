@@ -61,7 +61,10 @@ constexpr uint32_t kEntry = 144;   // stash entry stride: 128 B of state + 16 B 
                                    // consecutive slots start on different banks and the 8
                                    // pieces of an entry sit at immediate offsets
 constexpr uint32_t kImageBytes = 8192;
-constexpr uint32_t kWin1 = 12;    // window chunks (64 offsets each) loaded ahead of the first rows
+#ifndef LNL_SPAN_WIN1
+#define LNL_SPAN_WIN1 12u
+#endif
+constexpr uint32_t kWin1 = LNL_SPAN_WIN1;  // window chunks (64 offsets each) loaded ahead of the first rows
 
 #ifndef LNL_SPAN_PRIO
 #define LNL_SPAN_PRIO 0  // 0: progress-based issue priority; 1: static (experiment); 2: none

@@ -34,7 +34,9 @@ VARIANTS = {
     "span_treg1": "-DLNL_SPAN_TAIL_REG=1",          # ... folded in registers after a separate last flush (product: 2)
     "span_ffmask": "-DLNL_SPAN_F_MASK=1",           # span kernel: F(b) read by the boundary lanes only
     "span_ffmask_tl": "-DLNL_SPAN_F_MASK=1 -DLNL_SPAN_DIAG=16",
-    "span_finlds": "-DLNL_SPAN_FIN_LDS=1",          # span kernel: heads' final map from the LDS tables
+    "span_finlds": "-DLNL_SPAN_FIN_LDS=1",
+    "span_win9": "-DLNL_SPAN_WIN1=9u",              # span setup: 9 x 64 offsets in the first window (default 12)
+    "span_win16": "-DLNL_SPAN_WIN1=16u",          # span kernel: heads' final map from the LDS tables
     "span_nob": "-DLNL_SPAN_DIAG=32",               # span kernel, no batch kernel after it (overflow datagrams unwritten)
     "span_noprio": "-DLNL_SPAN_PRIO=2",            # span kernel: no issue-priority balancing
     "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
