@@ -23,10 +23,8 @@
 #include <vector>
 
 #include "../../include/lnl_crc32c.h"
-#include "crc32c_append.h"
 #include "crc32c_bitslice.h"
 #include "crc32c_kernels.h"
-#include "crc32c_seg.h"
 #include "crc32c_span.h"
 
 #ifndef LNL_EXPERIMENTS
@@ -79,9 +77,7 @@ struct DeviceState {
     std::string init_err;
     uint8_t* dummy = nullptr;  // 256 zero bytes of device memory
     uint32_t* fold = nullptr;  // kernel tables (lnl_build_tables), 12.5 KiB
-    uint32_t* pow = nullptr;   // segment kernel's row-power tables (lnl_build_seg_tables), 3.5 KiB
     uint32_t* span_tab = nullptr;  // span kernel's tables (lnl_build_span_tables), 145 KiB
-    uint32_t* append_tab = nullptr;  // outbound layer's tables (lnl_build_append_tables), 104 KiB
     int cus = 0;
     bool gfx950 = false;
     // host-path staging (guarded by host_mu)
@@ -113,26 +109,18 @@ int device_state(int dev, DeviceState** out) {
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(dev);
         static uint32_t host_fold[LNL_TABLE_WORDS];
-        static uint32_t host_pow[lnl::kSegPowTables * 128];
         static uint32_t host_span[lnl::kSpanTabWords];
-        static uint32_t host_app[lnl::kAppTabWords];
         static std::once_flag fold_once;
         std::call_once(fold_once, [] {
             lnl_build_tables(host_fold);
-            lnl_build_seg_tables(host_pow, (int)lnl::kSegPowTables);
             lnl::lnl_build_span_tables(host_span);
-            lnl::lnl_build_append_tables(host_app);
         });
         e = hipMalloc(&S.dummy, 256);
         if (e == hipSuccess) e = hipMemset(S.dummy, 0, 256);
         if (e == hipSuccess) e = hipMalloc(&S.fold, sizeof host_fold);
         if (e == hipSuccess) e = hipMemcpy(S.fold, host_fold, sizeof host_fold, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMalloc(&S.pow, sizeof host_pow);
-        if (e == hipSuccess) e = hipMemcpy(S.pow, host_pow, sizeof host_pow, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&S.span_tab, sizeof host_span);
         if (e == hipSuccess) e = hipMemcpy(S.span_tab, host_span, sizeof host_span, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMalloc(&S.append_tab, sizeof host_app);
-        if (e == hipSuccess) e = hipMemcpy(S.append_tab, host_app, sizeof host_app, hipMemcpyHostToDevice);
         // CSR / verify calls take their scratch from the stream-ordered pool
         // (hipMallocAsync / hipFreeAsync on the caller's stream).  Keep freed
         // blocks in the pool across synchronisations: with the default
@@ -541,24 +529,22 @@ int verify_csr(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t
 }  // namespace
 
 namespace {
-// The outbound layer over a device burst: the one-pass append kernel
-// (lnl_append.hip), CRCs into crc when it is not null.  (The experiments
-// build's two-pass form runs the CSR CRC pass into crc first.)
+// The outbound layer over a device burst: the CSR CRC pass into crc, then the
+// copy kernel (lnl_append.hip) writes the wire burst.
 int append_csr(const DeviceState& S, const lnl::BatchArgs& src, uint8_t* d_dst, uint32_t* crc, hipStream_t st) {
-    if (lnl::append_two_pass()) {
-        if (!crc) return fail(-EINVAL, "the two-pass append needs a CRC buffer");
-        lnl::BatchArgs a = src;
-        a.out = crc;
-        if (int rc = launch_csr(S, a, lnl::kModeCsr, st)) return rc;
-    }
-    lnl::AppendArgs p{src.base, src.off, src.n, d_dst, crc, src.off0, S.append_tab};
+    if (!crc) return fail(-EINVAL, "the append needs a CRC buffer");
+    lnl::BatchArgs a = src;
+    a.out = crc;
+    if (int rc = launch_csr(S, a, lnl::kModeCsr, st)) return rc;
+    lnl::AppendArgs p{src.base, src.off, src.n, d_dst, crc, src.off0};
     hipError_t e = lnl::launch_append(p, S.cus, st);
     return e == hipSuccess ? 0 : hip_fail(e, "append kernel launch");
 }
 }  // namespace
 
-// The outbound layer over a device burst: one pass over the payload bytes
-// (lnl_append.hip), the CRCs into d_crc when it is not null.
+// The outbound layer over a device burst: the CSR CRC pass, then the copy
+// kernel (lnl_append.hip); the CRCs into d_crc when it is not null (else into
+// stream-ordered scratch).
 extern "C" int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, uint8_t* d_dst,
                                          uint32_t* d_crc, void* hip_stream) {
     if (n == 0) return 0;
@@ -568,7 +554,7 @@ extern "C" int lnl_crc32c_append_csr_dev(const uint8_t* d_base, const uint64_t* 
     if (int rc = current_device(&S)) return rc;
     const hipStream_t st = (hipStream_t)hip_stream;
     uint32_t* crc = d_crc;
-    const bool scratch = !crc && lnl::append_two_pass();
+    const bool scratch = !crc;
     if (scratch) {
         hipError_t e = hipMallocAsync((void**)&crc, (size_t)n * sizeof(uint32_t), st);
         if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", (size_t)n * 4, hipGetErrorString(e));

@@ -137,23 +137,6 @@ LNL_HD inline void lnl_cols_inverse(const uint32_t* cols, uint32_t* inv) {
     }
 }
 
-// Row-power tables of the segment kernel (crc32c_seg.hip): table b is A^(2^b),
-// A = L^-1 step^1024 L -- one 128-byte row in the basis lnl_fold_tree's result
-// lives in -- as 8 nibble tables (128 words).  A fold result r of a prefix that
-// is followed by m more rows becomes A^m r.
-LNL_HD inline void lnl_build_seg_tables(uint32_t* t, int ntables) {
-    uint32_t L[32], Li[32], A[32], A2[32];
-    for (int k = 0; k < 32; ++k) L[k] = lnl_step_bits(LNL_CRC32C_POLY, 992 - 32 * k);
-    lnl_cols_inverse(L, Li);
-    for (int k = 0; k < 32; ++k) A[k] = lnl_cols_apply(Li, lnl_step_bits(L[k], 1024));
-    for (int b = 0; b < ntables; ++b) {
-        for (int k = 0; k < 8; ++k)
-            for (uint32_t v = 0; v < 16; ++v) t[b * 128 + k * 16 + v] = lnl_cols_apply(A, v << (4 * k));
-        for (int k = 0; k < 32; ++k) A2[k] = lnl_cols_apply(A, A[k]);
-        for (int k = 0; k < 32; ++k) A[k] = A2[k];
-    }
-}
-
 LNL_HD LNL_INLINE uint32_t lnl_table_b(uint32_t e) { return e & 15u; }
 LNL_HD LNL_INLINE uint32_t lnl_table_a(uint32_t e) { return 16u + (e >> 4); }
 

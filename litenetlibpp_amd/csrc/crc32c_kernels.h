@@ -128,23 +128,17 @@ void span_scratch_layout(SpanArgs& a, uint32_t* scratch, uint32_t parity);
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream);
 
 // Outbound layer over a device burst (lnl_append.hip): datagram i of the CSR
-// burst to dst + (off[i] - off[0]) + 4 i as payload || LE32(CRC): the team copy
-// after the CSR CRC pass (crc in), or -- experiments build, LNL_APPEND_MODE 1 --
-// in one pass over the payload (the team computes the CRCs from the registers
-// it copies, crc out; crc32c_append.h).
+// burst to dst + (off[i] - off[0]) + 4 i as payload || LE32(CRC), the CRCs
+// from the CSR CRC pass that runs first (crc in).
 struct AppendArgs {
     const uint8_t* base;
     const uint64_t* off;
     uint32_t n;
     uint8_t* dst;
-    uint32_t* crc;        // the CSR pass's CRCs (in); one-pass form: optional, out
+    const uint32_t* crc;  // the CSR pass's CRCs
     uint64_t off0;        // datagram i's bytes are base[off[i] - off0 ..) (host-path chunks: off0 = off[0])
-    const uint32_t* tab;  // kAppTabWords (lnl_build_append_tables)
 };
 hipError_t launch_append(const AppendArgs& a, int cus, hipStream_t stream);
-// the two-pass form (LNL_APPEND_MODE 0, the product, and 2: the CSR CRC pass into
-// crc, then the copy kernel): true when it is the one compiled in
-bool append_two_pass();
 
 // XOR-encryption layer over a batch (lnl_xor.hip), in place.
 constexpr uint32_t kXorMaxKey = 256;

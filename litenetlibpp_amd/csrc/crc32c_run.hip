@@ -32,8 +32,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <type_traits>
-
 #include "crc32c_device.h"
 #include "crc32c_kernels.h"
 
@@ -56,9 +54,6 @@ using namespace dev;
 constexpr int kWaves = kRunThreads / 64;
 constexpr int kBufsU4 = kWaves * 2 * kBufU4;  // the waves' row buffers
 constexpr int kFoldLdsU4 = kFoldU4 + 1;       // the tables + one uint4: per-wave progress words
-#ifndef LNL_RUN_VROWS
-#define LNL_RUN_VROWS 0  // 1: three rows in flight per wave (one by LDS-DMA, two through VGPRs; experiment)
-#endif
 #ifndef LNL_RUN_EARLY_ROWS
 #define LNL_RUN_EARLY_ROWS 1  // first rows issued before the tables land (0: after, as before round 3)
 #endif
@@ -149,254 +144,6 @@ __device__ LNL_INLINE uint32_t final_map(uint32_t fold_base, uint32_t e, uint32_
     return ~r;
 }
 
-#if LNL_RUN_VROWS
-// Experiment (tools/kvariants.py run3): THREE rows in flight per wave in the
-// same 16 KiB of LDS.  Rows t = 0 mod 3 come by LDS-DMA into buffer 0 as
-// above; rows t = 1, 2 mod 3 come into VGPRs (va, vb: the same pieces and
-// slots as the LDS-DMA loads, 64 registers) and are written into buffer 1 --
-// the image -- just before they are read.  Every row is 8 VMEM loads either
-// way, so the counted vmcnt waits stay exact.
-__device__ LNL_INLINE void issue_run_row_v(const RunBatch& B, uint32_t t, const uint32_t* off, uint32_t qs8,
-                                           u32x4* v) {
-    const uint64_t row = B.line + ((uint64_t)t << 7);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint64_t base = row + (uint64_t)i * qs8;
-        asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=v"(v[i]) : "v"(off[i & 1]), "s"(base) : "memory");
-    }
-}
-template <int I>
-struct ImageWrite {  // load i of a VGPR row to the image: the slot its LDS-DMA form would fill
-    __device__ static LNL_INLINE void write(uint32_t addr, const u32x4* v) {
-        asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v[I]), "i"(1024 * I) : "memory");
-        ImageWrite<I + 1>::write(addr, v);
-    }
-};
-template <>
-struct ImageWrite<8> {
-    __device__ static LNL_INLINE void write(uint32_t, const u32x4*) {}
-};
-#endif
-
-#if LNL_RUN_VROWS
-__global__ __launch_bounds__(kRunThreads, 512 / kRunThreads) void crc32c_run_kernel(RunArgs a) {
-    __shared__ __attribute__((aligned(128))) uint4 bufs[kBufsU4];
-    __shared__ __attribute__((aligned(16))) uint4 fold_arr[kFoldLdsU4];
-    const uint32_t lane = __lane_id();
-    const uint32_t wave = uni(threadIdx.x >> 6);
-    uint4* const buf_base = bufs + wave * (2 * kBufU4);
-    uint4* const fold_lds = fold_arr;
-    const uint32_t fold_base = (uint32_t)(uintptr_t)fold_lds;
-    uint32_t* const prog = reinterpret_cast<uint32_t*>(fold_lds + kFoldU4);
-    uint32_t rows_done = 0;
-    (void)prog;
-    (void)rows_done;
-    const uint32_t gw = blockIdx.x * kWaves + wave;
-    const uint32_t nw = gridDim.x * kWaves;
-    const bool active = gw < a.nb;
-
-    uint32_t off[2];
-    const uint32_t qs8 = 8u * a.q * (uint32_t)a.stride;
-    {
-        const uint32_t sub = lane >> 3, slot = lane & 7u;
-        off[0] = sub * a.q * (uint32_t)a.stride + 16u * (slot ^ swz(sub));
-        off[1] = sub * a.q * (uint32_t)a.stride + 16u * (slot ^ swz(sub) ^ 4u);
-    }
-    const uint32_t r0 = (uint32_t)(uintptr_t)(buf_base + lane * kRowU4) | (16u * swz(lane));
-    const uint32_t img = (uint32_t)(uintptr_t)(buf_base + kBufU4) + 16u * lane;
-    const uint32_t S = (uint32_t)a.stride, L = a.len, K = a.k;
-    const bool contiguous = S == L;
-
-    uint32_t wb = gw;
-    RunBatch cur{}, nxt{};
-    bool has_nxt = false;
-    uint32_t t = 0, inflight = 0;
-    u32x4 va[8], vb[8];
-    // row t + ahead of the wave's stream: of cur, or past its end of nxt
-    auto src = [&](uint32_t ahead, RunBatch& B, uint32_t& r) -> bool {
-        const uint32_t tt = t + ahead;
-        if (tt < cur.rows) {
-            B = cur;
-            r = tt;
-            return true;
-        }
-        if (has_nxt && tt - cur.rows < nxt.rows) {
-            B = nxt;
-            r = tt - cur.rows;
-            return true;
-        }
-        return false;
-    };
-    {
-        constexpr int kPer = (kFoldU4 + kRunThreads - 1) / kRunThreads;
-        u32x4 tv[kPer];
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = (int)threadIdx.x + j * kRunThreads;
-            const uint64_t at = (uint64_t)(uintptr_t)a.fold + 16u * (uint32_t)(i < kFoldU4 ? i : kFoldU4 - 1);
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(tv[j]) : "v"(at) : "memory");
-        }
-        if (active) {
-            cur = run_batch(a, wb);
-            has_nxt = wb + nw < a.nb;
-            if (has_nxt) nxt = run_batch(a, wb + nw);
-            RunBatch B;
-            uint32_t r;
-            if (src(0u, B, r)) {
-                issue_run_row(B, r, off, qs8, buf_base);
-                ++inflight;
-            }
-            if (src(1u, B, r)) {
-                issue_run_row_v(B, r, off, qs8, va);
-                ++inflight;
-            }
-            if (src(2u, B, r)) {
-                issue_run_row_v(B, r, off, qs8, vb);
-                ++inflight;
-            }
-        }
-        // the tables only (the rows are younger)
-        if (inflight >= 3u)
-            asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-        else if (inflight == 2u)
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else if (inflight == 1u)
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = (int)threadIdx.x + j * kRunThreads;
-            asm volatile("" : "+v"(tv[j]));
-            if (i < kFoldU4) lds_write_piece(fold_base + 16u * (uint32_t)i, tv[j]);
-        }
-        if (threadIdx.x == 0) lds_write_piece(fold_base + 16u * (uint32_t)kFoldU4, u32x4{0u, 0u, 0u, 0u});
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    }
-    if (!active) return;
-
-    uint32_t s[32], P[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) s[k] = P[k] = 0;
-    uint32_t ks = 0, ke = 0, sb = cur.ph, eb = cur.ph + L - 1u, eprev = 0;
-    uint32_t dl = cur.d0 + lane * a.q;
-
-    // the row's datagram boundaries and network (as the two-row kernel below)
-    auto consume = [&](uint32_t* x) {
-        const bool st = ks < K && (sb >> 7) == t;
-        const bool en = ke < K && (eb >> 7) == t;
-        if (!(st || en)) {
-            uint32_t o[32];
-            lnl_net_row_x(s, x, o);
-#pragma unroll
-            for (int k = 0; k < 32; ++k) s[k] = o[k];
-        } else if (!en) {
-            const uint32_t bs = sb & 127u;
-            MaskLoop<0>::apply<false>(x, s, start_mask(bs));
-            s[0] ^= lds_read_u32(fold_base + 4u * (LNL_TABLE_C_OFF + bs));
-            ++ks;
-            sb += S;
-        } else {
-            const uint32_t be = eb & 127u;
-            uint32_t o[32], xe[32];
-            MaskLoop<0>::apply<true>(x, xe, end_mask(be));
-            if (st) {
-                const uint32_t bs = sb & 127u;
-                if (contiguous) {
-#pragma unroll
-                    for (int w = 0; w < 32; ++w) x[w] ^= xe[w];
-                } else {
-                    MaskLoop<0>::apply<false>(x, x, start_mask(bs));
-                }
-                x[0] ^= lds_read_u32(fold_base + 4u * (LNL_TABLE_C_OFF + bs));
-                ++ks;
-                sb += S;
-            }
-            lnl_net_row_x(s, xe, o);
-            if (st) {
-#pragma unroll
-                for (int w = 0; w < 32; ++w) s[w] = x[w];
-            }
-            uint32_t f[32];
-            lnl_fold_level1(o, f);
-            if ((ke & 1u) == 0u) {
-#pragma unroll
-                for (int k = 0; k < 32; ++k) P[k] = f[k];
-                eprev = 127u - be;
-            } else {
-                uint32_t ra, rb;
-                lnl_fold_pair(P, f, ra, rb);
-                a.out[dl + ke - 1u] = final_map(fold_base, eprev, ra);
-                a.out[dl + ke] = final_map(fold_base, 127u - be, rb);
-            }
-            ++ke;
-            eb += S;
-        }
-    };
-    // one row step through ring slot SLOT (0: the LDS-DMA buffer, 1: va, 2: vb);
-    // false once the wave's last row is done
-    auto step = [&](auto slot_c) -> bool {
-        constexpr int SLOT = decltype(slot_c)::value;
-        if (inflight >= 3u)
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else if (inflight == 2u)
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint32_t x[32];
-        {
-            uint32_t rad[8], rb = r0;
-            asm volatile("" : "+v"(rb));
-#pragma unroll
-            for (int k = 0; k < 8; ++k) rad[k] = rb ^ (16u * k);
-            if constexpr (SLOT == 0) {
-                read_row<0>(rad, x);
-            } else if constexpr (SLOT == 1) {
-                ImageWrite<0>::write(img, va);
-                read_row<kBufBytes>(rad, x);
-            } else {
-                ImageWrite<0>::write(img, vb);
-                read_row<kBufBytes>(rad, x);
-            }
-        }
-        --inflight;
-        {
-            RunBatch B;
-            uint32_t r;
-            if (src(3u, B, r)) {
-                if constexpr (SLOT == 0)
-                    issue_run_row(B, r, off, qs8, buf_base);
-                else if constexpr (SLOT == 1)
-                    issue_run_row_v(B, r, off, qs8, va);
-                else
-                    issue_run_row_v(B, r, off, qs8, vb);
-                ++inflight;
-            }
-        }
-        consume(x);
-        if (++t == cur.rows) {
-            wb += nw;
-            if (!has_nxt) return false;
-            cur = nxt;
-            has_nxt = wb + nw < a.nb;
-            if (has_nxt) nxt = run_batch(a, wb + nw);
-            t = 0;
-            ks = ke = 0;
-            sb = cur.ph;
-            eb = cur.ph + L - 1u;
-            dl = cur.d0 + lane * a.q;
-        }
-        return true;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    while (step(I0{}) && step(I1{}) && step(I2{})) {
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-#else
 __global__ __launch_bounds__(kRunThreads, 512 / kRunThreads) void crc32c_run_kernel(RunArgs a) {
     // row buffers and tables in separate LDS arrays: the tables' LDS writes
     // then provably do not touch the LDS-DMA destinations, and the wait before
@@ -603,7 +350,6 @@ __global__ __launch_bounds__(kRunThreads, 512 / kRunThreads) void crc32c_run_ker
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-#endif  // LNL_RUN_VROWS
 
 }  // namespace
 

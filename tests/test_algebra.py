@@ -57,24 +57,6 @@ def test_kernel_lane_emulation(tmp_path):
     assert "bad=0" in r.stdout
 
 
-def test_segment_kernel_emulation(tmp_path):
-    """tests/emu/emu_seg.cpp: the CSR segment kernel's whole launch (pre-pass,
-    per-lane row events, head/tail combine, cross-wave fix-up, overflow list)
-    on the CPU, every datagram written exactly once with the oracle's CRC:
-    mixed 64..1400 B, tiny (segments with more ends than a lane tracks),
-    datagrams over many segments, lengths on line and segment boundaries,
-    empty datagrams, several wave counts and buffer offsets."""
-    oracle.load()
-    exe = tmp_path / "emu_seg"
-    src = os.path.join(ROOT, "tests", "emu", "emu_seg.cpp")
-    so_dir = os.path.dirname(oracle.ORACLE_SO)
-    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src, f"-L{so_dir}",
-                    "-lcrc32c_oracle", f"-Wl,-rpath,{so_dir}"], check=True)
-    r = subprocess.run([str(exe), "0.2"], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "bad=0" in r.stdout
-
-
 def test_span_fold_tables(tmp_path):
     """tests/emu/emu_span_fold.cpp: the span kernel's table-Horner fold and
     register-basis final map equal the bit-sliced fold tree and the batch
@@ -89,25 +71,3 @@ def test_span_fold_tables(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bad=0" in r.stdout
-
-
-def test_append_one_pass_emulation(tmp_path):
-    """tests/emu/emu_append.cpp: the one-pass outbound layer (crc32c_append.h)
-    -- destination-aligned pieces, C[pad] init, slicing-by-2 lane CRCs, the
-    512-byte Horner, per-lane shifts, team XOR and unshift -- gives the
-    oracle's CRC for every datagram, and the chunk-ownership rule writes every
-    wire byte exactly once (whole chunks where the owner knows all 16 bytes,
-    single bytes otherwise), for every destination alignment, lengths 0..80
-    alone and between neighbours, mixed bursts and 65,507-byte datagrams;
-    with the tables in 32 and in 16 copies, and the slicing-by-16 piece CRC."""
-    oracle.load()
-    src = os.path.join(ROOT, "tests", "emu", "emu_append.cpp")
-    so_dir = os.path.dirname(oracle.ORACLE_SO)
-    for repl, s16 in ((32, 0), (16, 0), (32, 1)):
-        exe = tmp_path / f"emu_append{repl}_{s16}"
-        subprocess.run(["g++", "-O2", "-std=c++17", f"-DLNL_APP_REPL={repl}", f"-DLNL_APP_SLICE16={s16}", "-o", str(exe),
-                        src, f"-L{so_dir}",
-                        "-lcrc32c_oracle", f"-Wl,-rpath,{so_dir}"], check=True)
-        r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0, r.stdout + r.stderr
-        assert "bad=0" in r.stdout

@@ -1,9 +1,10 @@
-"""The one-pass outbound layer (lnl_append.hip, crc32c_append.h) on the GPU:
-every shape the chunk-ownership rule distinguishes, at every destination
-alignment, with and without the CRC output; the wire burst checked byte for
-byte against lnl_crc32c_layer_outbound (the CPU layer) and the CRCs against
-the oracle.  (tests/test_gpu_parity.py holds the round-3 append cases and the
-full config-3 burst.)"""
+"""The outbound layer (lnl_crc32c_append_csr_dev: the CSR CRC pass, then
+lnl_append.hip's copy kernel) on the GPU: every shape of head chunk, whole
+chunks and tail (payload remainder + CRC) the copy distinguishes, at every
+destination alignment, with and without the CRC output; the wire burst checked
+byte for byte against lnl_crc32c_layer_outbound (the CPU layer) and the CRCs
+against the oracle.  (tests/test_gpu_parity.py holds the round-3 append cases
+and the full config-3 burst.)"""
 import numpy as np
 import pytest
 

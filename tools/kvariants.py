@@ -42,27 +42,13 @@ VARIANTS = {
     "span_prio_tl": "-DLNL_SPAN_PRIO=1 -DLNL_SPAN_DIAG=16",
     "span_timeline": "-DLNL_SPAN_DIAG=16",          # span kernel: per-wave timeline into out[] (wrong CRCs)
     "span_r3_tl": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0 -DLNL_SPAN_TAIL_REG=0 -DLNL_SPAN_DIAG=16",
-    "run3": "-DLNL_RUN_VROWS=1",                    # lane-run kernel: three rows in flight per wave (one LDS-DMA, two VGPR)
-    "run3_nt0": "-DLNL_RUN_VROWS=1 -DLNL_RUN_AUX=0",
     "run512": "-DLNL_RUN_THREADS=512",              # lane-run kernel: one 512-thread workgroup per CU
     "run512p": "-DLNL_RUN_THREADS=512 -DLNL_RUN_PRIO=1",  # ... with progress-based issue priority
-    "vpf0": "-DLNL_VERIFY_PREFETCH=0",            # verify / filter: trailing CRC + header read after the last row
-    "vpf1": "-DLNL_VERIFY_PREFETCH=1",            # ... when the batch is made
-    "app_dpp": "-DLNL_APPEND_COPY_DPP=1",           # outbound copy: aligned source chunks, neighbour's by DPP
     "app_u1": "-DLNL_APPEND_COPY_U=1",              # outbound layer: round 3's copy kernel (one chunk load in flight per lane)
     "app_u2": "-DLNL_APPEND_COPY_U=2",
     "app_u4": "-DLNL_APPEND_COPY_U=4",
-    "app_team": "-DLNL_APPEND_MODE=2",              # outbound layer: CSR CRC pass + the team copy (ownership rule)
-    "app_1pass": "-DLNL_APPEND_MODE=1",             # outbound layer in one pass (the team computes the CRCs)
-    "app_1pass_r16": "-DLNL_APPEND_MODE=1 -DLNL_APP_REPL=16",   # ... lane tables in 16 copies
-    "app_1pass_s16": "-DLNL_APPEND_MODE=1 -DLNL_APP_SLICE16=1",  # ... slicing-by-16 piece CRC
-    "app_1pass_t512": "-DLNL_APPEND_MODE=1 -DLNL_APPEND_THREADS=512",  # ... 512-thread workgroups (8 waves per CU)
-    "app_g2": "-DLNL_APPEND_GROUP=2",               # team kernels: pieces per lane loaded together (default 3)
-    "app_g4": "-DLNL_APPEND_GROUP=4",
     "app_w8": "-DLNL_APPEND_WGS=8u",                # copy kernel: workgroups per CU (default 16)
     "app_w32": "-DLNL_APPEND_WGS=32u",
-    "prep8k": "-DLNL_SPAN_PREP_BLOCKS=8192u",       # span pre-pass: 8192 workgroups (before: 1 % slower than 1024)
-    "prep256": "-DLNL_SPAN_PREP_BLOCKS=256u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
     "fix8": "-DLNL_SPAN_FIX_WGS=8u",                # ... 8 workgroups
     "fix1": "-DLNL_SPAN_FIX_WGS=1u",                # ... 1 workgroup
@@ -98,7 +84,9 @@ VARIANTS = {
     "k4q32": "-DLNL_RUN_K=4 -DLNL_RUN_QMIN=32",
     "run_dflt": "-DLNL_RUN_AUX=0",                  # default cache policy for the run kernel's loads
     "run_late": "-DLNL_RUN_EARLY_ROWS=0",           # run kernel: first rows issued after the tables land (before round 3)
-    # (round 1's uniform / segment / pair CSR paths: tools/experiments/csr_experiment_kernels.patch)
+    # (round 1's uniform / segment / pair CSR paths: tools/experiments/csr_experiment_kernels.patch;
+    #  round 4's one-pass append, three-row lane-run kernel and other removed shapes:
+    #  tools/experiments/round4_experiments.patch)
     "nobucket": "-DLNL_BUCKET_MIN_N=0xFFFFFFFFu",   # CSR: plain batch kernel, no pre-pass
     "bucket_atomic": "-DLNL_BUCKET_LAYOUT=0",       # CSR: atomic ranks, bucket after bucket (16 runs per bucket)
     "bucket_interleave": "-DLNL_BUCKET_LAYOUT=1",   # CSR: position-ordered buckets, batches interleaved by progress
