@@ -20,7 +20,12 @@
 //    caller sees the same sequence of accepted datagrams).
 //
 // REFNET_CRC=0 builds the same wrappers as pass-through observers (the CRC-off
-// baseline measured with identical plumbing).  Every variant records the
+// baseline measured with identical plumbing).  REFNET_CRC=2 (the crc_src
+// variant) also leaves the layer to the caller: there send_raw and
+// receive_logic themselves are rewritten to INTEGRATION.md's snippets
+// (build.py), so the wrappers only observe, corrupt, lose and inject; an
+// injected datagram gets its CRC here, since it replaces one that send_raw
+// had already checksummed.  Every variant records the
 // largest datagram it put on the wire, which is how the tests read the MTU the
 // probe settled on (net_peer keeps m_mtu private).  refnet_set_flip_every(n)
 // corrupts one bit of every n-th outgoing datagram after the CRC was written:
@@ -44,6 +49,9 @@
 
 #ifndef REFNET_CRC
 #define REFNET_CRC 1
+#endif
+#if REFNET_CRC == 2
+#include "refnet_layer.hpp"
 #endif
 
 extern "C" {
@@ -110,7 +118,19 @@ ssize_t __wrap_sendto(int fd, const void* buf, size_t len, int flags, const stru
     } done{injected};
 #if REFNET_CRC
     thread_local uint8_t scratch[65536 + LNL_CRC32C_LAYER_EXTRA];
+#if REFNET_CRC == 2
+    // the caller's datagram already carries its CRC; copied (the buffer is the
+    // caller's) so that a corrupting link can flip a bit of it
+    int64_t wire;
+    if (injected) {
+        wire = lnl_crc32c_layer_outbound((const uint8_t*)buf, 0, len, scratch, sizeof scratch);
+    } else {
+        wire = len <= sizeof scratch ? (int64_t)len : -1;
+        if (wire >= 0) memcpy(scratch, buf, len);
+    }
+#else
     const int64_t wire = lnl_crc32c_layer_outbound((const uint8_t*)buf, 0, len, scratch, sizeof scratch);
+#endif
     if (wire < 0) {
         errno = EMSGSIZE;
         return -1;
@@ -142,7 +162,7 @@ ssize_t __wrap_recvfrom(int fd, void* buf, size_t len, int flags, struct sockadd
         const ssize_t n = __real_recvfrom(fd, buf, len, flags, addr, alen ? &al : nullptr);
         if (n < 0) return n;
         if (alen) *alen = al;
-#if REFNET_CRC
+#if REFNET_CRC == 1
         const int64_t payload = lnl_crc32c_layer_inbound((const uint8_t*)buf, (size_t)n);
         if (payload < 0) {  // a checksum failure looks like loss to the reliability layer
             g_dropped.fetch_add(1, std::memory_order_relaxed);
@@ -158,10 +178,14 @@ ssize_t __wrap_recvfrom(int fd, void* buf, size_t len, int flags, struct sockadd
 }
 
 // observers for the test driver
-int refnet_crc_on(void) { return REFNET_CRC; }
+int refnet_crc_on(void) { return REFNET_CRC ? 1 : 0; }
 uint64_t refnet_sent(void) { return g_sent.load(); }
 uint64_t refnet_received(void) { return g_received.load(); }
+#if REFNET_CRC == 2
+uint64_t refnet_dropped(void) { return refnet_layers_dropped(); }  // the rewritten receive_logic's layers
+#else
 uint64_t refnet_dropped(void) { return g_dropped.load(); }
+#endif
 uint64_t refnet_flipped(void) { return g_flipped.load(); }
 int64_t refnet_max_sent(void) { return g_max_sent.load(); }
 void refnet_reset_max_sent(void) { g_max_sent.store(0); }

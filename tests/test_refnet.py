@@ -18,6 +18,9 @@ box has no /root/reference, so everything here skips there.
   the layer.
 * A link that corrupts one datagram in five: the layer drops every corrupted
   one (counted) and RELIABLE_ORDERED still delivers all 300 messages in order.
+* The same with INTEGRATION.md's send_raw / receive_logic snippets applied as
+  source text (variant crc_src: the reference's net_manager.cpp is rewritten
+  in a pipe, nothing copied; the socket wrappers only observe).
 """
 import json
 import os
@@ -56,21 +59,21 @@ def drive(built, variant, *args, timeout=120):
     return res
 
 
-@pytest.mark.parametrize("variant", ["crc", "plain"])
+@pytest.mark.parametrize("variant", ["crc", "crc_src", "plain"])
 @pytest.mark.parametrize("test", ["connect", "send_receive"])
 def test_reference_tests_recreated(built, variant, test):
     res = drive(built, variant, test)
-    assert res["crc"] == (variant == "crc")
+    assert res["crc"] == (variant != "plain")
     assert res["dropped"] == 0
 
 
-@pytest.mark.parametrize("variant", ["crc", "plain"])
+@pytest.mark.parametrize("variant", ["crc", "crc_src", "plain"])
 def test_reference_example_echo(built, variant):
     res = drive(built, variant, "echo")
     assert res["typed_echoed"] == 25 and res["fragment_echoed"] == 1
 
 
-@pytest.mark.parametrize("variant", ["crc", "plain"])
+@pytest.mark.parametrize("variant", ["crc", "crc_src", "plain"])
 def test_reference_example_processes(built, variant):
     """The example's own two executables connect through the layer (the
     handshake datagrams carry CRCs) and echo traffic back.  How many of the 25
@@ -114,7 +117,7 @@ def test_reference_example_processes(built, variant):
     assert cnt or "TestFrag" in sout, (out, sout)
 
 
-@pytest.mark.parametrize("variant,mtu", [("crc", 1428), ("crc_nomtu", 1424), ("plain", 1432)])
+@pytest.mark.parametrize("variant,mtu", [("crc", 1428), ("crc_src", 1428), ("crc_nomtu", 1424), ("plain", 1432)])
 def test_mtu_probe_settles(built, variant, mtu):
     res = drive(built, variant, "mtu", timeout=60)
     assert res["mtu"] == mtu, res
@@ -123,8 +126,12 @@ def test_mtu_probe_settles(built, variant, mtu):
         assert res["dropped"] > 0  # the truncated 1436-byte probes
 
 
-def test_bit_flipping_link(built):
-    res = drive(built, "crc", "flip", "5", timeout=60)
+@pytest.mark.parametrize("variant", ["crc", "crc_src"])
+def test_bit_flipping_link(built, variant):
+    """crc: the layer at the socket calls (link-time wrappers); crc_src: the
+    INTEGRATION.md edits in send_raw / receive_logic themselves, where a dropped
+    datagram is recycled and the loop goes back to its poll."""
+    res = drive(built, variant, "flip", "5", timeout=60)
     assert res["received"] == 300 and res["in_order"]
     assert res["dropped"] == res["flipped"] > 0  # every corrupted datagram, and nothing else
 
