@@ -292,15 +292,6 @@ int lnl_stream_release(void* hip_stream);
  * pair by per-call epoch, crc32c_span.h). */
 int lnl_diag_fill_span_arrivals(void* hip_stream, uint64_t value);
 
-/* Diagnostics (tests): the fused filter + dispatch call's look-back scratch
- * kept for `hip_stream` (lnl_dispatch.hip dispatch_walked_kernel): fills every
- * workgroup flag with `fill`, as an aborted call could leave them, and sets the
- * stream's call count to `calls` (the next call's flag epoch is
- * (calls + 1) mod 2^30; at 0 the flags are zeroed first).  Synchronises the
- * stream first; blocking.  -ENOENT when no fused call has run on the stream.
- * Later calls must be unaffected unless `fill` carries their epoch. */
-int lnl_diag_look_scratch(void* hip_stream, uint64_t calls, uint64_t fill);
-
 /* Message for the last failure on the calling thread ("" if none). */
 const char* lnl_crc32c_last_error(void);
 

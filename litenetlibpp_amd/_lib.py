@@ -113,8 +113,6 @@ def lib() -> ctypes.CDLL:
     L.lnl_stream_release.argtypes = [ctypes.c_void_p]
     L.lnl_diag_fill_span_arrivals.restype = ctypes.c_int
     L.lnl_diag_fill_span_arrivals.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    L.lnl_diag_look_scratch.restype = ctypes.c_int
-    L.lnl_diag_look_scratch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
     L.lnl_crc32c_last_error.restype = ctypes.c_char_p
     L.lnl_crc32c_last_error.argtypes = []
     L.lnl_crc32c_abi_version.restype = ctypes.c_int

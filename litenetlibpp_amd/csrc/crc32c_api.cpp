@@ -205,6 +205,9 @@ int csr_path() {
 
 #endif  // LNL_EXPERIMENTS
 
+#ifndef LNL_DISPATCH_SCAN
+#define LNL_DISPATCH_SCAN 0  // 1: the hipCUB scan between the dispatch passes at every size (round 4; experiments)
+#endif
 #ifndef LNL_SPAN_ROUNDS
 #define LNL_SPAN_ROUNDS 1u  // wave-batches per resident wave the segment length is chosen for (experiments)
 #endif
@@ -254,7 +257,6 @@ struct SpanScratch {
     uint32_t* buf = nullptr;
     size_t words = 0;
     uint64_t calls = 0;  // span path: calls made on it (the control block parity and the exchange epoch)
-    uint64_t tickets = 0;  // look-back scratch: workgroup tickets taken by the calls made on it
     uint64_t used = 0;   // LRU tick
 };
 
@@ -281,7 +283,6 @@ struct ScratchCache {
                 return hip_fail(e, "hipMemsetAsync");
             s.words = grow;
             s.calls = 0;
-            s.tickets = 0;
         }
         *out = &s;
         evict(key);
@@ -324,32 +325,6 @@ int span_scratch(hipStream_t st, size_t words, size_t zero_words, SpanScratch** 
 // the span scratch: each call's map kernel rewrites the words its XOR kernel
 // reads, in stream order, so calls on one stream share it.
 ScratchCache g_xor_cache;
-
-// The fused dispatch's look-back scratch (lnl_dispatch.hip
-// dispatch_walked_kernel), kept per (device, stream) like the span scratch:
-// [0] the workgroup ticket counter, then a flag per workgroup, all zeroed when
-// allocated.  Calls on one stream take consecutive epochs and tickets, so no
-// call resets anything; when the 30-bit epoch would wrap to 0 (the zeroed
-// flags' epoch) the flags are zeroed again first.  The cache's mutex is held
-// through the launch (launch order = epoch order).
-ScratchCache g_look_cache;
-
-int look_scratch(hipStream_t st, uint32_t n, lnl::DispatchArgs& a, SpanScratch** out) {
-    const size_t words = lnl::dispatch_look_words(n);
-    SpanScratch* s = nullptr;
-    if (int rc = g_look_cache.get(st, words, words, &s)) return rc;
-    constexpr uint64_t kMask = (1ull << lnl::kLookEpochBits) - 1ull;
-    if (((s->calls + 1u) & kMask) == 0u) {
-        hipError_t e = hipMemsetAsync(s->buf + 2, 0, (s->words - 2) * sizeof(uint32_t), st);
-        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-        ++s->calls;
-    }
-    a.lb = reinterpret_cast<uint64_t*>(s->buf);
-    a.epoch = (uint32_t)((s->calls + 1u) & kMask);
-    a.ticket0 = s->tickets;
-    *out = s;
-    return 0;
-}
 
 int xor_map_scratch(hipStream_t st, size_t words, uint32_t** buf) {
     std::lock_guard<std::mutex> lk(g_xor_cache.mu);
@@ -470,7 +445,6 @@ extern "C" const char* lnl_crc32c_last_error(void) { return g_err.c_str(); }
 extern "C" int lnl_stream_release(void* hip_stream) {
     g_span_cache.release((hipStream_t)hip_stream);
     g_xor_cache.release((hipStream_t)hip_stream);
-    g_look_cache.release((hipStream_t)hip_stream);
     return 0;
 }
 
@@ -489,23 +463,6 @@ extern "C" int lnl_diag_fill_span_arrivals(void* hip_stream, uint64_t value) {
     uint32_t* xch = it->second.buf + 2 * lnl::kSpanCtlWords + lnl::kSpanXchFlag;  // (span_scratch_layout)
     e = hipMemcpy2D(xch, lnl::kSpanXchWords * 4u, v.data(), 8, 8, blocks, hipMemcpyHostToDevice);
     return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpy2D");
-}
-
-extern "C" int lnl_diag_look_scratch(void* hip_stream, uint64_t calls, uint64_t fill) {
-    const hipStream_t st = (hipStream_t)hip_stream;
-    DeviceState* S;
-    if (int rc = current_device(&S)) return rc;
-    std::lock_guard<std::mutex> lk(g_look_cache.mu);
-    auto it = g_look_cache.m.find(stream_key(st));
-    if (it == g_look_cache.m.end() || !it->second.buf) return fail(-ENOENT, "no look-back scratch kept for this stream");
-    SpanScratch& s = it->second;
-    hipError_t e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-    std::vector<uint64_t> v((s.words - 2) / 2, fill);
-    e = hipMemcpy(s.buf + 2, v.data(), v.size() * 8, hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
-    s.calls = calls;
-    return 0;
 }
 
 extern "C" int lnl_crc32c_abi_version(void) { return LNL_CRC32C_ABI_VERSION; }
@@ -900,7 +857,11 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
         if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
         return rc;
     }
-    const size_t scan_bytes = lnl::dispatch_scan_bytes(n);
+    // batches of up to kDispatchPrefixWgs workgroups: per-workgroup totals
+    // (the emit pass sums its predecessors'); larger: a hipCUB scan into first
+    const uint32_t nwg = (uint32_t)(((size_t)n + 255) / 256);
+    const bool prefix = nwg <= lnl::kDispatchPrefixWgs && !LNL_DISPATCH_SCAN;
+    const size_t scan_bytes = prefix ? 0 : lnl::dispatch_scan_bytes(n);
     void* scratch = nullptr;
     const size_t bytes = (2 + (size_t)lnl::kDispatchRec) * n * 4 + scan_bytes + 256;
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
@@ -911,7 +872,8 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     a.n = n;
     a.status = d_status;
     a.counts = (uint32_t*)scratch;
-    a.first = a.counts + n;
+    a.first = a.counts + n;  // (prefix: its first nwg words are the workgroup totals)
+    a.wgsum = prefix ? a.first : nullptr;
     a.rec = a.first + n;
     a.nt = nt_stores;
     a.pkt_start = d_pkt_start;
@@ -952,16 +914,11 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
         return lnl_dispatch_csr_dev(d_base, d_off, n, d_status, d_pkt_start, d_pkt_len, d_pkt_parent, cap, d_total,
                                     hip_stream);
     }
-#if LNL_EXPERIMENTS && defined(LNL_DISPATCH_WALKED3)
-    constexpr bool three = true;  // round 4's fix-up + hipCUB scan + emit (A/B, tools/kvariants.py fd3)
-#else
-    constexpr bool three = false;
-#endif
-    const size_t scan_bytes = three ? lnl::dispatch_scan_bytes(n) : 0;
+    const uint32_t nwg = (uint32_t)(((size_t)n + 255) / 256);
+    const bool prefix = nwg <= lnl::kDispatchPrefixWgs && !LNL_DISPATCH_SCAN;
+    const size_t scan_bytes = prefix ? 0 : lnl::dispatch_scan_bytes(n);
     void* scratch = nullptr;
-    // walk blocks (+ counts, first, records and the scan's temporary for the three-launch form)
-    const size_t bytes = three ? (2 + (size_t)lnl::kDispatchRec + lnl::kWalkBlock) * n * 4 + scan_bytes + 512
-                               : (size_t)lnl::kWalkBlock * n * 4;
+    const size_t bytes = (2 + (size_t)lnl::kDispatchRec + lnl::kWalkBlock) * n * 4 + scan_bytes + 512;
     hipError_t e = hipMallocAsync(&scratch, bytes, st);
     if (e != hipSuccess) return fail(-ENOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
     lnl::DispatchArgs a{};
@@ -969,21 +926,18 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     a.off = d_off;
     a.n = n;
     a.status = d_status;
+    a.counts = (uint32_t*)scratch;
+    a.first = a.counts + n;  // (prefix: its first nwg words are the workgroup totals)
+    a.wgsum = prefix ? a.first : nullptr;
+    a.rec = a.first + n;
     a.pkt_start = d_pkt_start;
     a.pkt_len = d_pkt_len;
     a.pkt_parent = d_pkt_parent;
     a.cap = cap;
     a.total = d_total;
-    uint32_t* blk = (uint32_t*)scratch;
-    void* tmp = nullptr;
-    if (three) {
-        a.counts = (uint32_t*)scratch;
-        a.first = a.counts + n;
-        a.rec = a.first + n;
-        blk = (uint32_t*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);
-        tmp = (void*)(((uintptr_t)(blk + (size_t)lnl::kWalkBlock * n) + 255) & ~(uintptr_t)255);
-    }
+    uint32_t* blk = (uint32_t*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);
     a.blk = blk;
+    void* tmp = (void*)(((uintptr_t)(blk + (size_t)lnl::kWalkBlock * n) + 255) & ~(uintptr_t)255);
     lnl::BatchArgs b{};
     b.base = d_base;
     b.off = d_off;
@@ -993,21 +947,8 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     const uint32_t* span_ctl = nullptr;
     int rc = launch_csr_span(*S, b, st, lnl::kSpanFilter, blk, &span_ctl);
     a.span_ctl = span_ctl;  // [2] != 0: the span kernel walked the batch
-    if (rc == 0 && three) {
-#if LNL_EXPERIMENTS
-        if ((e = lnl::launch_dispatch_walked3(a, tmp, scan_bytes, st)) != hipSuccess) rc = hip_fail(e, "dispatch launch");
-#endif
-    } else if (rc == 0) {
-        std::lock_guard<std::mutex> lk(g_look_cache.mu);
-        SpanScratch* ls = nullptr;
-        rc = look_scratch(st, n, a, &ls);
-        if (rc == 0 && (e = lnl::launch_dispatch_walked(a, st)) != hipSuccess) rc = hip_fail(e, "dispatch launch");
-        if (rc == 0) {  // (the launch took the epoch and its workgroups' tickets)
-            ++ls->calls;
-            ls->tickets += ((uint64_t)n + 255u) / 256u;
-        }
-    }
-    (void)tmp;
+    if (rc == 0 && (e = lnl::launch_dispatch_walked(a, tmp, scan_bytes, st)) != hipSuccess)
+        rc = hip_fail(e, "dispatch launch");
     e = hipFreeAsync(scratch, st);
     if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
     return rc;

@@ -200,30 +200,22 @@ struct DispatchArgs {
     // control block ([2] != 0: the span kernel took the batch and walked it)
     const uint32_t* blk;
     const uint32_t* span_ctl;
-    // fused path, one launch (dispatch_walked_kernel): the stream's look-back
-    // scratch -- [0] a u64 workgroup ticket counter, then one u64 flag per
-    // workgroup (epoch << 34 | state << 32 | value) -- this call's epoch
-    // (1 .. 2^30 - 1) and the ticket counter's value when the call starts
-    uint64_t* lb;
-    uint32_t epoch;
-    uint64_t ticket0;
+    // two-launch form (batches of at most kDispatchPrefixWgs workgroups): the
+    // count / fix-up pass leaves each 256-datagram workgroup's packet total
+    // here and the emit pass sums its predecessors' (no scan launch; first is
+    // unused).  Null: the hipCUB scan of counts into first.
+    uint32_t* wgsum;
 };
+constexpr uint32_t kDispatchPrefixWgs = 8192;
 constexpr uint32_t kDispatchRec = 8;  // packets per datagram kept from the counting walk
 constexpr uint32_t kWalkBlock = 8;             // fused path: words per datagram block [count, 7 records]
 constexpr uint32_t kWalkPlain = 0x80000000u;    // block count: not a container, one packet
 size_t dispatch_scan_bytes(uint32_t n);
 hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
-// Fused path (lnl_inbound_filter_dispatch_csr_dev): one launch turns the span
+// Fused path (lnl_inbound_filter_dispatch_csr_dev): the fix-up turns the span
 // kernel's walk blocks into counts + records (zero for datagrams not
-// accepted; walking again only what the blocks cannot hold), finds each
-// workgroup's first output slot by a decoupled look-back over a.lb, and emits
-// the packets as above.
-constexpr uint32_t kLookEpochBits = 30;
-size_t dispatch_look_words(uint32_t n);  // u32 words of a.lb for a batch of n datagrams
-hipError_t launch_dispatch_walked(const DispatchArgs& a, hipStream_t stream);
-#if LNL_EXPERIMENTS
-// round 4's three launches (fix-up, hipCUB scan, emit), for A/B measurements
-hipError_t launch_dispatch_walked3(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
-#endif
+// accepted; walking again only what the blocks cannot hold), then scan + emit
+// as above.
+hipError_t launch_dispatch_walked(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream);
 
 }  // namespace lnl

@@ -25,16 +25,15 @@
 // A nested container is delivered as one packet (the reference's
 // process_packet would cut it again); send_merged never nests.
 //
-// Two launches around a device-wide exclusive scan (hipCUB): walk and count
-// the packets of every datagram (recording the first kDispatchRec), then emit
-// them in datagram order from the records.  A walk step is one dependent
-// round trip to a random 64-B sector, so walking each container once (not
-// once per pass) halves the latency-bound part of the call.
-//
-// The fused path (lnl_inbound_filter_dispatch_csr_dev, whose span kernel has
-// already walked the containers) is one launch: dispatch_walked_kernel reads
-// the walk blocks, finds its output range by a decoupled look-back over
-// per-workgroup flags and emits.
+// Two launches: walk and count the packets of every datagram (recording the
+// first kDispatchRec), then emit them in datagram order from the records.  A
+// walk step is one dependent round trip to a random 64-B sector, so walking
+// each container once (not once per pass) halves the latency-bound part of
+// the call.  The emit pass finds datagram i's first output slot itself: the
+// counting pass leaves each workgroup's packet total, and an emit workgroup
+// adds up its predecessors' totals (at most kDispatchPrefixWgs of them, read
+// from L2) and scans its own counts.  Larger batches run a hipCUB exclusive
+// scan of the counts between the two launches instead.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -91,30 +90,45 @@ __device__ inline uint32_t walk(const DispatchArgs& a, uint64_t s, uint32_t size
     return c;
 }
 
+// Sum of v over the 256-thread workgroup (every thread calls it; uses a
+// barrier).
+__device__ inline uint32_t block_sum(uint32_t v, uint32_t* s_part) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
+    if (lane == 0u) s_part[w] = v;
+    __syncthreads();
+    return s_part[0] + s_part[1] + s_part[2] + s_part[3];
+}
+
 // Pass 1: walk every accepted datagram once; count its packets and keep the
 // first kDispatchRec as (pos << 16 | len) records, slot-major so a wave's
 // stores are coalesced.
 __global__ __launch_bounds__(256) void dispatch_count_kernel(DispatchArgs a) {
+    __shared__ uint32_t s_part[4];
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= a.n) return;
     uint32_t c = 0;
-    const uint8_t st = a.status[i];  // issued together with the offsets
-    const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
-    if (st == 1u) {  // LNL_INBOUND_ACCEPT only
-        const uint64_t s = o0 - a.off0;
-        const uint32_t size = (uint32_t)(o1 - o0) - 4u;  // CRC stripped
-        uint32_t k = 0;
-        c = walk(a, s, size, [&](uint32_t pos, uint32_t len) {
-            if (k < kDispatchRec) a.rec[(size_t)k * a.n + i] = (pos << 16) | len;
-            ++k;
-        });
+    if (i < a.n) {
+        const uint8_t st = a.status[i];  // issued together with the offsets
+        const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
+        if (st == 1u) {  // LNL_INBOUND_ACCEPT only
+            const uint64_t s = o0 - a.off0;
+            const uint32_t size = (uint32_t)(o1 - o0) - 4u;  // CRC stripped
+            uint32_t k = 0;
+            c = walk(a, s, size, [&](uint32_t pos, uint32_t len) {
+                if (k < kDispatchRec) a.rec[(size_t)k * a.n + i] = (pos << 16) | len;
+                ++k;
+            });
+        }
+        a.counts[i] = c;
     }
-    a.counts[i] = c;
+    if (a.wgsum) {
+        const uint32_t t = block_sum(c, s_part);
+        if (threadIdx.x == 0u) a.wgsum[blockIdx.x] = t;
+    }
 }
 
-#if LNL_EXPERIMENTS
-// Pass 1 of round 4's fused path (experiments build: launch_dispatch_walked3;
-// the product runs dispatch_walked_kernel below): the span kernel left one block per datagram
+// Pass 1 of the fused path: the span kernel left one block per datagram
 // ([count, records 0 .. 6], written by the lane that owns the datagram; a
 // block per datagram keeps those scattered writes to one 32-byte sector).
 // Keep the counts of accepted datagrams, zero the rest, move the records to
@@ -122,9 +136,9 @@ __global__ __launch_bounds__(256) void dispatch_count_kernel(DispatchArgs a) {
 // what a block cannot hold (8 or more packets) or what the span kernel did not
 // see (a batch it does not take: its control block says so).
 __global__ __launch_bounds__(256) void dispatch_fix_kernel(DispatchArgs a) {
+    __shared__ uint32_t s_part[4];
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= a.n) return;
-    const uint8_t st = a.status[i];
+    const uint8_t st = i < a.n ? a.status[i] : 0u;
     uint32_t c = 0;
     if (st == 1u) {
         const bool walked = a.span_ctl[2] != 0u;  // (written by the span kernel of this call)
@@ -150,9 +164,12 @@ __global__ __launch_bounds__(256) void dispatch_fix_kernel(DispatchArgs a) {
             });
         }
     }
-    a.counts[i] = c;
+    if (i < a.n) a.counts[i] = c;
+    if (a.wgsum) {
+        const uint32_t t = block_sum(c, s_part);
+        if (threadIdx.x == 0u) a.wgsum[blockIdx.x] = t;
+    }
 }
-#endif
 
 // Pass 2: datagram i's packets go to [first[i], first[i] + counts[i]).  A
 // wave owns 64 consecutive datagrams, whose packets form one contiguous range
@@ -168,12 +185,39 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
     __shared__ uint32_t s_fast[4][64];
     __shared__ uint64_t s_start[4][64];
     __shared__ uint32_t s_rec[4][kDispatchRec][64];
+    __shared__ uint32_t s_part[4], s_wsum[4];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t i0 = blockIdx.x * 256u + w * 64u;
     const uint32_t i = i0 + lane;
     uint32_t c = 0, f = 0, size = 0;
     uint64_t s = 0;
-    if (i < a.n) {
+    if (a.wgsum) {
+        // first slot = the predecessors' totals + this workgroup's scan
+        uint32_t pre = 0;  // (8 loads in flight per thread: <= 4 round trips for 8192 workgroups)
+        for (uint32_t t = threadIdx.x; t < blockIdx.x; t += 8u * 256u) {
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8u; ++j) v[j] = t + 256u * j < blockIdx.x ? a.wgsum[t + 256u * j] : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < 8u; ++j) pre += v[j];
+        }
+        c = i < a.n ? a.counts[i] : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= (uint32_t)d) incl += o;
+        }
+        if (lane == 63u) s_wsum[w] = incl;
+        pre = block_sum(pre, s_part);  // (its barrier also publishes s_wsum)
+        for (uint32_t v = 0; v < w; ++v) pre += s_wsum[v];
+        f = pre + incl - c;  // lanes past n: c = 0, f = the total
+        if (i < a.n) {
+            if (i + 1u == a.n) *a.total = f + c;
+            s = a.off[i] - a.off0;
+            if (c) size = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
+        }
+    } else if (i < a.n) {
         c = a.counts[i];
         f = a.first[i];
         if (i + 1u == a.n) *a.total = f + c;
@@ -210,191 +254,6 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
                 a.pkt_len[j] = r & 0xFFFFu;
                 a.pkt_parent[j] = i0 + lo;
             }
-        }
-    }
-    if (c == 0u || f >= a.cap || (coop && fast)) return;
-    auto put = [&](uint32_t k, uint32_t pos, uint32_t len) {
-        if (f + k < a.cap) {
-            a.pkt_start[f + k] = s + pos;
-            a.pkt_len[f + k] = len;
-            a.pkt_parent[f + k] = i;
-        }
-    };
-    if (fast) {
-        for (uint32_t k = 0; k < c; ++k) {
-            const uint32_t r = s_rec[w][k][lane];
-            put(k, r >> 16, r & 0xFFFFu);
-        }
-    } else {
-        uint32_t k = 0;
-        walk(a, s, size, [&](uint32_t pos, uint32_t len) { put(k++, pos, len); });
-    }
-}
-
-// ---- decoupled look-back ---------------------------------------------------
-// Flags are read and written at agent scope (the per-XCD L2s are not coherent:
-// these go to memory), one u64 per workgroup.  A flag carries its whole
-// payload (the value and the epoch in the one word), so nothing else is
-// ordered through it: relaxed agent-scope accesses, with no L2 writeback
-// before each store and no invalidate after each poll.
-__device__ inline uint64_t flag_load(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void flag_store(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Fused path, one launch (replaces round 4's fix-up + hipCUB scan + emit, 45 us
-// per config-1-shaped call in three launches and an init kernel).
-//  * Workgroup order: each workgroup takes a ticket (a u64 counter in the
-//    stream's look-back scratch that only ever grows) and works on datagrams
-//    [256 b, 256 b + 256) for b = ticket - a.ticket0.  Every workgroup it
-//    waits on took an earlier ticket, so it is resident or done: the spin
-//    below always ends (it is bounded anyway; a timeout reports total =
-//    0xFFFFFFFF instead of hanging).
-//  * Counts and records: dispatch_fix_kernel's rules (span kernel blocks;
-//    walk again what a block cannot hold), into LDS.
-//  * Offsets: the workgroup scans its 256 counts, publishes its aggregate
-//    (state 1), and wave 0 sums its predecessors' values 64 flags per round
-//    trip back to the nearest inclusive prefix (state 2); then it publishes
-//    its own.  A flag carries the call's epoch: a flag left by an earlier call
-//    reads as unpublished, so the flags are never reset (zeroed once, when the
-//    scratch is allocated, and again when the 30-bit epoch wraps).
-//  * Emit: dispatch_emit_kernel's cooperative stores.
-constexpr uint32_t kLookSpinMax = 1u << 20;  // polls (~1 s) before a workgroup gives up
-constexpr uint64_t kLookEpochMask = (1ull << kLookEpochBits) - 1ull;
-
-__device__ inline uint64_t look_word(uint32_t epoch, uint32_t state, uint32_t value) {
-    return ((uint64_t)epoch << 34) | ((uint64_t)state << 32) | value;
-}
-__device__ inline uint32_t look_state(uint64_t v, uint32_t epoch) {
-    return (v >> 34) == (uint64_t)epoch ? (uint32_t)(v >> 32) & 3u : 0u;
-}
-
-__global__ __launch_bounds__(256) void dispatch_walked_kernel(DispatchArgs a) {
-    __shared__ uint32_t s_first[4][65];
-    __shared__ uint32_t s_fast[4][64];
-    __shared__ uint64_t s_start[4][64];
-    __shared__ uint32_t s_rec[4][kDispatchRec][64];
-    __shared__ uint32_t s_wsum[4];
-    __shared__ uint32_t s_prefix, s_bad, s_b;
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    uint64_t* const flags = a.lb + 1;
-    if (threadIdx.x == 0u)
-        s_b = (uint32_t)(atomicAdd(reinterpret_cast<unsigned long long*>(a.lb), 1ull) - a.ticket0);
-    __syncthreads();
-    const uint32_t b = s_b;
-    if (b >= gridDim.x) return;  // (the host keeps ticket0 in step with the counter; never taken)
-    const uint32_t i0 = b * 256u + w * 64u;
-    const uint32_t i = i0 + lane;
-    uint32_t c = 0, size = 0;
-    uint64_t s = 0;
-    if (i < a.n) {
-        const uint8_t st = a.status[i];
-        const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
-        s = o0 - a.off0;
-        if (st == 1u) {  // LNL_INBOUND_ACCEPT only
-            size = (uint32_t)(o1 - o0) - 4u;  // CRC stripped
-            const bool walked = a.span_ctl[2] != 0u;  // (written by the span kernel of this call)
-            const uint4* blk = reinterpret_cast<const uint4*>(a.blk + (size_t)i * kWalkBlock);
-            const uint4 b0 = walked ? blk[0] : make_uint4(kWalkBlock, 0u, 0u, 0u);
-            c = b0.x;
-            if (c == kWalkPlain) {  // the datagram itself (a record only when size < 2^16: fast below)
-                s_rec[w][0][lane] = size;
-                c = 1;
-            } else if (c < kWalkBlock) {
-                const uint4 b1 = blk[1];
-                const uint32_t r[7] = {b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-                for (uint32_t k = 0; k < 7; ++k)
-                    if (k < c) s_rec[w][k][lane] = r[k];
-            } else {
-                uint32_t k = 0;
-                c = walk(a, s, size, [&](uint32_t pos, uint32_t len) {
-                    if (k < kDispatchRec) s_rec[w][k][lane] = (pos << 16) | len;
-                    ++k;
-                });
-            }
-        }
-    }
-    const bool fast = c <= kDispatchRec && size < 65536u;
-    // the workgroup's scan of its counts: waves by shuffles, then the 4 wave sums
-    uint32_t incl = c;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
-        if (lane >= (uint32_t)d) incl += o;
-    }
-    if (lane == 63u) s_wsum[w] = incl;
-    __syncthreads();
-    uint32_t wbase = 0, total = 0;
-#pragma unroll
-    for (uint32_t v = 0; v < 4u; ++v) {
-        wbase += v < w ? s_wsum[v] : 0u;
-        total += s_wsum[v];
-    }
-    if (w == 0u) {  // wave 0 looks back, 64 predecessors per round trip
-        const uint32_t ep = a.epoch;
-        uint32_t prefix = 0, bad = 0;
-        if (b == 0u) {
-            if (lane == 0u) flag_store(&flags[0], look_word(ep, 2u, total));
-        } else {
-            if (lane == 0u) flag_store(&flags[b], look_word(ep, 1u, total));
-            int64_t j = (int64_t)b - 1;
-            uint32_t spin = 0;
-            while (true) {
-                const int64_t idx = j - (int64_t)lane;
-                const uint64_t v = idx >= 0 ? flag_load(&flags[idx]) : look_word(ep, 2u, 0u);  // before 0: prefix 0
-                const uint32_t state = look_state(v, ep);
-                const uint64_t m2 = __ballot(state == 2u), m0 = __ballot(state == 0u);
-                const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
-                const uint64_t need = first2 >= 63u ? ~0ull : ((2ull << first2) - 1ull);
-                if (m0 & need) {  // a predecessor this window needs has not published yet
-                    if (++spin > kLookSpinMax) {
-                        bad = 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                uint32_t part = lane <= first2 ? (uint32_t)v : 0u;
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) part += (uint32_t)__shfl_xor((int)part, d, 64);
-                prefix += part;
-                if (first2 < 64u) break;
-                j -= 64;
-            }
-            if (lane == 0u && !bad) flag_store(&flags[b], look_word(ep, 2u, prefix + total));
-        }
-        if (lane == 0u) {
-            s_prefix = prefix;
-            s_bad = bad;
-        }
-    }
-    __syncthreads();
-    const uint32_t f = s_prefix + wbase + incl - c;  // first output slot of datagram i
-    if (i + 1u == a.n) *a.total = s_bad ? 0xFFFFFFFFu : f + c;
-    if (s_bad) return;
-    // cooperative, coalesced write of the wave's packets (dispatch_emit_kernel)
-    s_first[w][lane] = f;  // lanes past n: c = 0, f = the running total
-    if (lane == 63u) s_first[w][64] = f + c;
-    s_fast[w][lane] = fast;
-    s_start[w][lane] = s;
-    __syncthreads();
-    if (i0 >= a.n) return;
-    const uint32_t F0 = s_first[w][0], F1 = s_first[w][64];
-    const bool coop = F1 - F0 <= kEmitMaxSteps * 64u;
-    if (coop) {
-        const uint32_t end = F1 < a.cap ? F1 : a.cap;
-        for (uint32_t j = F0 + lane; j < end; j += 64u) {
-            uint32_t lo = 0;  // last datagram d of the wave with first[d] <= j
-            for (uint32_t step = 32; step; step >>= 1)
-                if (s_first[w][lo + step] <= j && lo + step < 64u) lo += step;
-            if (!s_fast[w][lo]) continue;
-            const uint32_t r = s_rec[w][j - s_first[w][lo]][lo];
-            a.pkt_start[j] = s_start[w][lo] + (r >> 16);
-            a.pkt_len[j] = r & 0xFFFFu;
-            a.pkt_parent[j] = i0 + lo;
         }
     }
     if (c == 0u || f >= a.cap || (coop && fast)) return;
@@ -579,6 +438,7 @@ size_t dispatch_scan_bytes(uint32_t n) {
 
 hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream) {
     const dim3 grid((a.n + 255u) / 256u);
+    if (a.wgsum && grid.x > kDispatchPrefixWgs) return hipErrorInvalidValue;
 #if LNL_EXPERIMENTS
     if (a.look) {  // one pass (flags zeroed by the caller)
         hipLaunchKernelGGL(dispatch_onepass_kernel, grid, dim3(256), 0, stream, a);
@@ -590,31 +450,26 @@ hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_by
     hipLaunchKernelGGL(dispatch_count_kernel, grid, dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, a.counts, a.first, (int)a.n, stream);
-    if (e != hipSuccess) return e;
+    if (!a.wgsum) {
+        e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, a.counts, a.first, (int)a.n, stream);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(dispatch_emit_kernel, grid, dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
-size_t dispatch_look_words(uint32_t n) { return 2u * (1u + ((size_t)n + 255u) / 256u); }
-
-hipError_t launch_dispatch_walked(const DispatchArgs& a, hipStream_t stream) {
-    if (!a.lb || a.epoch == 0u || a.epoch > kLookEpochMask) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(dispatch_walked_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, stream, a);
-    return hipGetLastError();
-}
-
-#if LNL_EXPERIMENTS
-hipError_t launch_dispatch_walked3(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream) {
+hipError_t launch_dispatch_walked(const DispatchArgs& a, void* scan_tmp, size_t scan_bytes, hipStream_t stream) {
     const dim3 grid((a.n + 255u) / 256u);
+    if (a.wgsum && grid.x > kDispatchPrefixWgs) return hipErrorInvalidValue;
     hipLaunchKernelGGL(dispatch_fix_kernel, grid, dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, a.counts, a.first, (int)a.n, stream);
-    if (e != hipSuccess) return e;
+    if (!a.wgsum) {
+        e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, a.counts, a.first, (int)a.n, stream);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(dispatch_emit_kernel, grid, dim3(256), 0, stream, a);
     return hipGetLastError();
 }
-#endif
 
 }  // namespace lnl

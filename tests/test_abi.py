@@ -40,7 +40,7 @@ def test_header_declares_the_boundary():
               "lnl_dispatch_csr_dev", "lnl_inbound_filter_dispatch_csr_dev", "lnl_xor_layer", "lnl_xor_layer_csr_dev", "lnl_xor_layer_fixed_dev",
               "lnl_crc32c_append_host", "lnl_egress_send_batch", "lnl_crc32c_batch_host_ex",
               "lnl_inbound_filter_host_ex", "lnl_crc32c_append_host_ex", "lnl_stream_release",
-              "lnl_diag_fill_span_arrivals", "lnl_diag_look_scratch"):
+              "lnl_diag_fill_span_arrivals"):
         assert s in syms
 
 

@@ -809,45 +809,35 @@ def test_filter_dispatch_fused_edges(P):
         assert int((status == 1).sum()) == n
 
 
-def test_filter_dispatch_fused_lookback_scratch(P):
-    """The fused call's emit is one launch that finds each workgroup's output
-    range by a decoupled look-back over per-workgroup flags, kept per stream
-    across calls and never reset: calls of different sizes in a row, flags
-    holding whatever an aborted call could leave, and the 30-bit flag epoch's
-    wrap all give the two calls' statuses and packets."""
-    rng = np.random.default_rng(777)
-    layer = P.Crc32cLayer()
-    sub = lambda m: bytes([0x00]) + rng.integers(0, 256, m - 1, dtype=np.uint8).tobytes()
-
-    def batch(n):
-        wires = [bytes(layer.process_outbound(_merged(rng, [sub(int(rng.integers(1, 300)))
-                                                            for _ in range(int(rng.integers(0, 9)))], "ok")))
-                 for _ in range(n)]
-        off = np.concatenate([[0], np.cumsum([len(w) for w in wires])]).astype(np.int64)
-        return dev(np.frombuffer(b"".join(wires) + bytes(8), np.uint8)), dev(off, torch.int64)
-
-    batches = [batch(n) for n in (40000, 17000, 90000)]
-    ref = []
-    for d, o in batches:
-        st2 = P.inbound_filter(d, o)
-        ref.append((st2,) + tuple(P.dispatch(d, o, st2)))
-
-    def check_all(rounds=1):
-        for _ in range(rounds):
-            for (d, o), r in zip(batches, ref):
-                got = P.filter_dispatch(d, o)
-                assert all(torch.equal(a, b) for a, b in zip(got, r))
-
-    check_all(3)  # sizes alternate: the ticket base and the epochs carry over
-    s = torch.cuda.current_stream().cuda_stream
-    L = P.lib()
-    # stale flags: epochs 5, 2^30 - 1 and 0 (with states 2, 3 and 1); the next calls use 101 ..
-    for fill in (0, 0xFFFFFFFFFFFFFFFF, (5 << 34) | (2 << 32) | 123, (1 << 32) | 7):
-        assert L.lnl_diag_look_scratch(s, 100, fill) == 0, L.lnl_crc32c_last_error()
-        check_all()
-    # the wrap: epochs 2^30 - 2, 2^30 - 1, then the flags are zeroed and epochs restart at 1
-    assert L.lnl_diag_look_scratch(s, (1 << 30) - 3, (((1 << 30) - 5) << 34) | (2 << 32) | 9) == 0
-    check_all(2)
+def test_dispatch_totals_and_scan_paths_agree(P):
+    """Batches of up to kDispatchPrefixWgs x 256 = 2 Mi datagrams find their
+    output slots from per-workgroup totals (the emit pass adds up its
+    predecessors'); larger ones run a hipCUB scan between the passes.  A
+    2.2 M-datagram batch (scan) delivers exactly its two halves' packets
+    (totals), for the standalone and the fused call."""
+    rng = np.random.default_rng(99)
+    n = 2_200_000
+    ent = lambda k: b"".join(bytes([3, 0, 0, 0x40 + k, 0x41]) for _ in range(k))  # [u16 3][UNRELIABLE, 2 B]
+    templates = [bytes([0x0C]) + ent(k) for k in range(5)] + [bytes([0x00]) + bytes(m) for m in (0, 3, 17)]
+    pick = rng.integers(0, len(templates), n)
+    payload = np.frombuffer(b"".join(templates[j] for j in pick) + bytes(8), np.uint8)
+    lens = np.array([len(t) for t in templates], np.int64)[pick]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    wire = P.append_csr(dev(payload), dev(off, torch.int64))
+    woff = dev(off + 4 * np.arange(n + 1, dtype=np.int64), torch.int64)
+    status = P.inbound_filter(wire, woff)
+    assert int((status == 1).sum()) == n
+    full = P.dispatch(wire, woff, status)
+    h = n // 2
+    a = P.dispatch(wire, woff[:h + 1], status[:h])
+    b = P.dispatch(wire, woff[h:], status[h:])
+    assert torch.equal(full[0], torch.cat([a[0], b[0]]))
+    assert torch.equal(full[1], torch.cat([a[1], b[1]]))
+    assert torch.equal(full[2], torch.cat([a[2], b[2] + h]))
+    assert full[0].numel() == int(np.array([0, 1, 2, 3, 4, 1, 1, 1])[pick].sum())
+    fst, fs, fl, fp = P.filter_dispatch(wire, woff)
+    assert torch.equal(fst, status)
+    assert torch.equal(fs, full[0]) and torch.equal(fl, full[1]) and torch.equal(fp, full[2])
 
 
 def test_filter_dispatch_fused_several_batches_per_wave(P):

@@ -69,7 +69,7 @@ VARIANTS = {
     "xgrid_dflt": "-DLNL_XOR_CSR_NT=0",             # ... default cache policy
     "xcsr_prev": "",                                # A/B slot: built from another lnl_xor.hip copied in by hand             # CSR XOR: the per-datagram kernel (before)
     "span_r2": "-DLNL_SPAN_ROUNDS=2u",              # CSR span: segments for two wave-batches per wave (static)
-    "fd3": "-DLNL_DISPATCH_WALKED3",                 # fused filter + dispatch: round 4's fix-up + scan + emit (product: one launch)
+    "disp_scan": "-DLNL_DISPATCH_SCAN=1",           # dispatch passes with the hipCUB scan between them (before: product sums workgroup totals)
     "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)
     "walk_noend": "-DLNL_WALK_DIAG=2",              # ... no walk at datagram ends (wrong packets)
     "walk_notail": "-DLNL_WALK_DIAG=4",             # ... no global-memory finish (wrong packets)
