@@ -69,6 +69,12 @@ struct HostSlot {
     uint32_t* d_out = nullptr;
     uint8_t* d_wire = nullptr;  // append: the chunk's wire burst
     size_t cap_bytes = 0, cap_n = 0, cap_wire = 0;
+    // pinned staging for a chunk's small results (CRCs / statuses) when the
+    // caller's output array is pageable, and where they go once the chunk is done
+    uint8_t* h_stage = nullptr;
+    size_t cap_stage = 0;
+    void* pend_dst = nullptr;
+    size_t pend_bytes = 0;
 };
 
 struct DeviceState {
@@ -665,6 +671,16 @@ int slot_ready(HostSlot& s, size_t need_bytes, size_t need_n, size_t need_wire) 
         s.cap_bytes = nb;
         s.cap_n = need_n;
     }
+    if (need_n * 4 > s.cap_stage) {  // pinned result staging (used for pageable outputs)
+        (void)hipHostFree(s.h_stage);
+        s.h_stage = nullptr;
+        s.cap_stage = 0;
+        if ((e = hipHostMalloc((void**)&s.h_stage, need_n * 4, hipHostMallocDefault)) != hipSuccess)
+            return fail(-ENOMEM, "pinned staging allocation: %s", hipGetErrorString(e));
+        s.cap_stage = need_n * 4;
+    }
+    s.pend_dst = nullptr;
+    s.pend_bytes = 0;
     if (need_wire > s.cap_wire) {  // the wire staging: append calls only
         (void)hipFree(s.d_wire);
         s.d_wire = nullptr;
@@ -676,6 +692,31 @@ int slot_ready(HostSlot& s, size_t need_bytes, size_t need_n, size_t need_wire) 
     return 0;
 }
 
+// Page-locked (hipHostMalloc / hipHostRegister) host memory: the DMA engines
+// copy into it directly.  Into pageable memory a D2H goes through the runtime's
+// own staging and holds up the pipeline (config 5 with a pageable CRC array:
+// 50.2 against 53.9 GB/s, tools/host_path_probe.py).
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // (pageable memory: an error, not sticky)
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+// A slot's staged results of its previous chunk to the caller's array (the
+// chunk is done once its stream is)
+int host_unstage(HostSlot& s) {
+    if (!s.pend_bytes) return 0;
+    hipError_t e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    memcpy(s.pend_dst, s.h_stage, s.pend_bytes);
+    s.pend_dst = nullptr;
+    s.pend_bytes = 0;
+    return 0;
+}
+
 int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h_out, int device,
                uint32_t mode, uint32_t* h_crc, const lnl_host_opts* opts) {
     HostPlan plan;
@@ -683,8 +724,14 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
     if (n == 0) return 0;
     if (!h_base || !h_off || !h_out) return fail(-EINVAL, "NULL argument");
     const uint32_t filter = mode == kHostFilter;
-    for (uint32_t i = 0; i < n; ++i)
-        if (h_off[i + 1] < h_off[i]) return fail(-EINVAL, "offsets decrease at %u", i);
+    {
+        // (branch-free, so it vectorises: this runs before the first copy is queued)
+        bool bad = false;
+        for (uint32_t i = 0; i < n; ++i) bad |= h_off[i + 1] < h_off[i];
+        if (bad)
+            for (uint32_t i = 0; i < n; ++i)
+                if (h_off[i + 1] < h_off[i]) return fail(-EINVAL, "offsets decrease at %u", i);
+    }
     DeviceState* S;
     if (int rc = device_state(device, &S)) return rc;
     std::lock_guard<std::mutex> lk(S->host_mu);
@@ -700,10 +747,14 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
     const int ns = plan.streams;
     // chunk boundaries: <= chunk_n datagrams and <= chunk_bytes bytes (a single
     // larger datagram gets a chunk of its own)
+    // (a binary search over the non-decreasing offsets: the last j <= i +
+    // chunk_n with off[j] - off[i] <= chunk_bytes)
     auto chunk_end = [&](uint32_t i) {
-        uint32_t j = i + 1;
-        while (j < n && j - i < plan.chunk_n && h_off[j + 1] - h_off[i] <= plan.chunk_bytes) ++j;
-        return j;
+        const uint32_t hi = (uint32_t)std::min<uint64_t>(n, (uint64_t)i + std::max<uint32_t>(plan.chunk_n, 1u));
+        const uint64_t lim = plan.chunk_bytes > UINT64_MAX - h_off[i] ? UINT64_MAX : h_off[i] + plan.chunk_bytes;
+        const uint64_t* p = std::upper_bound(h_off + i + 1, h_off + hi + 1, lim);
+        const uint32_t j = (uint32_t)(p - h_off) - 1u;
+        return j > i ? j : i + 1u;
     };
     size_t need_bytes = 0;
     uint32_t need_n = 0;
@@ -719,9 +770,16 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
     // after the first enqueue, every error path drains the streams first: the
     // caller may free h_base / h_out as soon as we return
     auto drained = [&](int rc) {
-        for (int s2 = 0; s2 < ns; ++s2) (void)hipStreamSynchronize(S->slot[s2].stream);
+        for (int s2 = 0; s2 < ns; ++s2) {
+            (void)hipStreamSynchronize(S->slot[s2].stream);
+            S->slot[s2].pend_bytes = 0;
+        }
         return rc;
     };
+    // the small result arrays (CRCs, statuses, append's optional CRCs) go
+    // through the slots' pinned staging when the caller's are pageable
+    void* const small_out = mode == kHostAppend ? (void*)h_crc : h_out;
+    const bool stage = small_out && !host_pinned(small_out);
     uint32_t i = 0;
     int k = 0;
     while (i < n) {
@@ -730,6 +788,7 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         const size_t cb = h_off[j] - h_off[i];
         HostSlot& s = S->slot[k];
         hipStream_t st = s.stream;
+        if (int rc = host_unstage(s)) return drained(rc);  // (its previous chunk: done by now, the others in flight)
         if (cb && (e = hipMemcpyAsync(s.d_bytes, h_base + h_off[i], cb, hipMemcpyHostToDevice, st)) != hipSuccess)
             return drained(hip_fail(e, "H2D bytes"));
         if ((e = hipMemcpyAsync(s.d_off, h_off + i, (size_t)(cn + 1) * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
@@ -748,9 +807,15 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
             if ((e = hipMemcpyAsync(dst, s.d_wire, cb + (size_t)cn * LNL_CRC32C_LAYER_EXTRA, hipMemcpyDeviceToHost,
                                     st)) != hipSuccess)
                 return drained(hip_fail(e, "D2H wire"));
-            if (h_crc && (e = hipMemcpyAsync(h_crc + i, s.d_out, (size_t)cn * 4, hipMemcpyDeviceToHost, st)) !=
-                             hipSuccess)
-                return drained(hip_fail(e, "D2H crc"));
+            if (h_crc) {
+                void* to = stage ? (void*)s.h_stage : (void*)(h_crc + i);
+                if ((e = hipMemcpyAsync(to, s.d_out, (size_t)cn * 4, hipMemcpyDeviceToHost, st)) != hipSuccess)
+                    return drained(hip_fail(e, "D2H crc"));
+                if (stage) {
+                    s.pend_dst = h_crc + i;
+                    s.pend_bytes = (size_t)cn * 4;
+                }
+            }
         } else {
             if (filter) {
                 a.ok = (uint8_t*)s.d_out;
@@ -760,16 +825,23 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
                 a.out = s.d_out;
                 if (int rc = launch_csr(*S, a, lnl::kModeCsr, st)) return drained(rc);
             }
-            if ((e = hipMemcpyAsync((uint8_t*)h_out + (size_t)i * esz, s.d_out, (size_t)cn * esz,
+            uint8_t* const dst = (uint8_t*)h_out + (size_t)i * esz;
+            if ((e = hipMemcpyAsync(stage ? (void*)s.h_stage : (void*)dst, s.d_out, (size_t)cn * esz,
                                     hipMemcpyDeviceToHost, st)) != hipSuccess)
                 return drained(hip_fail(e, "D2H"));
+            if (stage) {
+                s.pend_dst = dst;
+                s.pend_bytes = (size_t)cn * esz;
+            }
         }
         i = j;
         k = (k + 1) % ns;
     }
-    for (int s = 0; s < ns; ++s)
+    for (int s = 0; s < ns; ++s) {
         if ((e = hipStreamSynchronize(S->slot[s].stream)) != hipSuccess)
             return drained(hip_fail(e, "hipStreamSynchronize"));
+        if (int rc = host_unstage(S->slot[s])) return drained(rc);
+    }
     return 0;
 }
 }  // namespace

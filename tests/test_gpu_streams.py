@@ -72,6 +72,31 @@ def test_host_crc_stream_counts(P, streams):
     assert np.array_equal(P.batch_host(pinned, off, 0, streams=streams), oracle.batch_csr(data, off))
 
 
+def test_host_outputs_pinned_and_pageable(P):
+    """The host pipeline's small results (CRCs, statuses) go straight into a
+    page-locked output array and through the slots' pinned staging into a
+    pageable one (copied out as each slot is reused and at the end): both
+    equal the oracle, several chunks per stream."""
+    import ctypes
+    data, off = csr_batch(901, 70_001, shift=1)
+    pinned = torch.from_numpy(data).pin_memory().numpy()
+    exp = oracle.batch_csr(data, off)
+    opts = P.HostOpts.make(streams=2, chunk_datagrams=4096)
+    n = off.size - 1
+    for out in (np.zeros(n, np.uint32), torch.zeros(n, dtype=torch.int32).pin_memory().numpy().view(np.uint32)):
+        rc = P.lib().lnl_crc32c_batch_host_ex(pinned.ctypes.data, off.ctypes.data, n, out.ctypes.data, 0,
+                                              ctypes.pointer(opts))
+        assert rc == 0, P.lib().lnl_crc32c_last_error()
+        assert np.array_equal(out, exp)
+    wd, woff, wexp = wire_batch(P, 902, 30_000)
+    wpinned = torch.from_numpy(wd).pin_memory().numpy()
+    for st in (np.full(woff.size - 1, 9, np.uint8), torch.full((woff.size - 1,), 9, dtype=torch.uint8).pin_memory().numpy()):
+        rc = P.lib().lnl_inbound_filter_host_ex(wpinned.ctypes.data, woff.ctypes.data, woff.size - 1, st.ctypes.data,
+                                                0, ctypes.pointer(opts))
+        assert rc == 0, P.lib().lnl_crc32c_last_error()
+        assert np.array_equal(st, wexp)
+
+
 @pytest.mark.parametrize("streams", [2, 4])
 def test_host_filter_stream_counts(P, streams):
     data, off, exp = wire_batch(P, 600 + streams, 40_000)
