@@ -855,7 +855,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             uint32_t slot = tail_slot + rank;
             slot = slot >= kCap ? slot - kCap : slot;
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 8)
+            if (false) {  // diagnostic build only: no stash writes (wrong CRCs)
+#else
             if (take) {
+#endif
                 Pieces<0>::write(stash + slot * kEntry, P, F);
                 const uint2 mt = make_uint2(k, info);
                 asm volatile("ds_write_b64 %0, %1" ::"v"(meta + slot * 8u), "v"(mt) : "memory");
@@ -905,7 +909,11 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 uint32_t ad[8];
 #pragma unroll
                 for (int p = 0; p < 8; ++p) ad[p] = (uint32_t)p < bp ? zero_addr : r0 ^ (16u * p);
-#if LNL_SPAN_F_MASK
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 4)
+                (void)ad;  // diagnostic build only: no F(b) read (wrong CRCs)
+#pragma unroll
+                for (int w = 0; w < 32; ++w) F[w] = 0u;
+#elif LNL_SPAN_F_MASK
                 // only the lanes with a boundary read F: a row's other lanes
                 // would move 128 bytes each through the LDS for nothing
                 if (ev) read_row<0>(ad, F);
@@ -1046,6 +1054,9 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             }
             refill();
             ev = is_open() && Q.front() <= rowend;
+#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 64)
+            ev = false;  // diagnostic build only: a row's second and later boundaries skipped (wrong CRCs)
+#endif
             while (__any(ev)) {
                 const uint32_t b = ev ? Q.front() - rowst : 128u;
                 const bool zero = ev && cs == (int32_t)(rowst + b);  // empty datagram: CRC 0, too short for the layer

@@ -74,8 +74,9 @@ VARIANTS = {
     "walk_noend": "-DLNL_WALK_DIAG=2",              # ... no walk at datagram ends (wrong packets)
     "walk_notail": "-DLNL_WALK_DIAG=4",             # ... no global-memory finish (wrong packets)
     "walk_none": "-DLNL_WALK_DIAG=7",               # ... none of the three (wrong packets)
-    "span_noflush": "-DLNL_SPAN_DIAG=4",            # CSR span kernel: stash entries dropped unread (wrong CRCs)
-    "span_noput": "-DLNL_SPAN_DIAG=12",             # ... and not written either (wrong CRCs)
+    "span_noF": "-DLNL_SPAN_DIAG=4",                # CSR span kernel: boundaries without the F(b) read (wrong CRCs)
+    "span_noput": "-DLNL_SPAN_DIAG=8",              # ... without the stash writes (wrong CRCs)
+    "span_nob2": "-DLNL_SPAN_DIAG=64",              # ... a row's second and later boundaries skipped (wrong CRCs)
     "bucketed": ("", 4),                            # CSR: the bucketed batch kernel (previous default)
     "batch": "-DLNL_NO_RUN",                        # any-layout batch kernel for everything
     "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
