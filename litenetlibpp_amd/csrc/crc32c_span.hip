@@ -94,9 +94,6 @@ constexpr uint32_t kWin1 = LNL_SPAN_WIN1;  // window chunks (64 offsets each) lo
 #ifndef LNL_SPAN_F_MASK
 #define LNL_SPAN_F_MASK 0  // 1: F(b) read by the lanes with a boundary only (experiment)
 #endif
-#ifndef LNL_SPAN_PRE2
-#define LNL_SPAN_PRE2 0  // 1: a row's second boundary piece read with the row too (CRC / filter kernels; experiment)
-#endif
 #ifndef LNL_SPAN_FIN_LDS
 #define LNL_SPAN_FIN_LDS 0  // 1: the heads' final map from the LDS tables (TB, TA), not the global FIN table
 #endif
@@ -881,8 +878,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
         // with state F(b) ^ C[b].  F(b) = the row from byte b on: b's piece
         // AND-masked in place in the image, earlier pieces from a zero piece.
         // (pre: the lane's piece b >> 4 as read with the row, or null: read here)
-        auto boundary = [&](uint32_t t, bool ev, bool zero, uint32_t b, bool take, uint32_t* sout, const u32x4* pre,
-                            bool pre_ok = true, u32x4* pre_next = nullptr) {
+        auto boundary = [&](uint32_t t, bool ev, bool zero, uint32_t b, bool take, uint32_t* sout, const u32x4* pre) {
             {
                 const uint32_t nst = (uint32_t)__popcll(__ballot(take));
                 const uint32_t cnt = st_tail - st_head;
@@ -896,7 +892,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint64_t lo = d < 8u ? ~0ull << (8u * d) : 0ull;
                 const uint64_t hi = d < 8u ? ~0ull : ~0ull << (8u * (d - 8u));
                 const uint32_t m[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-                if (pre && pre_ok) {
+                if (pre) {
                     u32x4 v = *pre;
                     v.x &= m[0];
                     v.y &= m[1];
@@ -917,13 +913,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 (void)ad;  // diagnostic build only: no F(b) read (wrong CRCs)
 #pragma unroll
                 for (int w = 0; w < 32; ++w) F[w] = 0u;
-#elif LNL_SPAN_PRE2
-                if (pre_next) {  // (the next boundary's piece, after this one's patch: masking it again is the same)
-                    const uint32_t b2 = (Q.q[0] >> 16) - ((t << 7));
-                    read_row_pre(ad, r0 ^ (16u * ((b2 >> 4) & 7u)), F, *pre_next);
-                } else {
-                    read_row<0>(ad, F);
-                }
 #elif LNL_SPAN_F_MASK
                 // only the lanes with a boundary read F: a row's other lanes
                 // would move 128 bytes each through the LDS for nothing
@@ -954,8 +943,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 inj = b == 128u ? 0xFFFFFFFFu : 0u;  // C[0] at the next row's word 0
                 if (A.mode != kSpanCrc) {  // the new datagram's first byte (intact after the patch)
                     hdr_next = b == 128u;
-                    if (b < 128u)
-                        chdr = pre && pre_ok ? piece_byte(*pre, b) : lds_read_u8((r0 ^ (16u * (b >> 4))) + (b & 15u));
+                    if (b < 128u) chdr = pre ? piece_byte(*pre, b) : lds_read_u8((r0 ^ (16u * (b >> 4))) + (b & 15u));
                 }
             }
 #pragma unroll
@@ -1038,12 +1026,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 #endif
             const uint32_t b = ev ? Q.front() - rowst : 128u;
             u32x4 pre;  // the piece holding b, read with the row (no separate round trip to mask it)
-#if LNL_SPAN_PRE2
-            // the piece of the lane's next boundary in this row, read with the
-            // first boundary's F(b) (valid when the queue held that entry: a
-            // refill after the first boundary brings new entries, qn = 16)
-            u32x4 pre2;
-#endif
             {
                 uint32_t x[32], rad[8], rr = r0;
                 asm volatile("" : "+v"(rr));  // 7 XORs per row rather than 8 registers held
@@ -1066,14 +1048,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             {
                 const bool take = ev && cs >= -(int32_t)Sb;  // (a row's first boundary never ends an empty datagram)
                 if constexpr (WALK) walk_end(t, ev, b);
-#if LNL_SPAN_PRE2
-                if constexpr (!WALK)
-                    boundary(t, ev, false, b, take, sout, &pre, true, &pre2);
-                else
-                    boundary(t, ev, false, b, take, sout, &pre);
-#else
                 boundary(t, ev, false, b, take, sout, &pre);
-#endif
                 if constexpr (WALK)
                     if (ev && b < 128u) walk_open();
             }
@@ -1081,9 +1056,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
             ev = is_open() && Q.front() <= rowend;
 #if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 64)
             ev = false;  // diagnostic build only: a row's second and later boundaries skipped (wrong CRCs)
-#endif
-#if LNL_SPAN_PRE2
-            bool second = true;
 #endif
             while (__any(ev)) {
                 const uint32_t b = ev ? Q.front() - rowst : 128u;
@@ -1093,16 +1065,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     store_result(A, k, 0u, 0u, 0u);
                 }
                 if constexpr (WALK) walk_end(t, ev, b);
-#if LNL_SPAN_PRE2
-                if constexpr (!WALK) {
-                    boundary(t, ev, zero, b, take, sout, &pre2, second && qn < 16u);
-                    second = false;
-                } else {
-                    boundary(t, ev, zero, b, take, sout, nullptr);
-                }
-#else
                 boundary(t, ev, zero, b, take, sout, nullptr);
-#endif
                 if constexpr (WALK)
                     if (ev && b < 128u) walk_open();
                 refill();

@@ -76,7 +76,7 @@ VARIANTS = {
     "walk_none": "-DLNL_WALK_DIAG=7",               # ... none of the three (wrong packets)
     "span_noF": "-DLNL_SPAN_DIAG=4",                # CSR span kernel: boundaries without the F(b) read (wrong CRCs)
     "span_noput": "-DLNL_SPAN_DIAG=8",              # ... without the stash writes (wrong CRCs)
-    "span_pre2": "-DLNL_SPAN_PRE2=1",               # span kernel: a row's second boundary piece read with the row
+    # (span_pre2, a row's second boundary piece read with the first boundary's F(b): commit 1545e07, measured no gain, removed)
     "span_nob2": "-DLNL_SPAN_DIAG=64",              # ... a row's second and later boundaries skipped (wrong CRCs)
     "bucketed": ("", 4),                            # CSR: the bucketed batch kernel (previous default)
     "batch": "-DLNL_NO_RUN",                        # any-layout batch kernel for everything
