@@ -113,7 +113,6 @@ struct SpanArgs {
     uint32_t* xch;           // per wave-batch boundary: exchange block (crc32c_span.h kSpanXch*)
     uint64_t epoch;          // this call's exchange epoch (>= 1, one per call on the scratch)
     uint32_t* ovf;           // n: datagrams left to the batch kernel
-    uint2* stage;            // n: CRC mode, the flushes' {datagram, CRC} pairs, wave-batch by wave-batch (8-byte aligned)
     // verify modes (kSpanVerify, kSpanFilter): ok[i] instead of out[i]
     uint32_t mode;
     uint8_t* ok;

@@ -94,12 +94,6 @@ constexpr uint32_t kWin1 = LNL_SPAN_WIN1;  // window chunks (64 offsets each) lo
 #ifndef LNL_SPAN_F_MASK
 #define LNL_SPAN_F_MASK 0  // 1: F(b) read by the lanes with a boundary only (experiment)
 #endif
-#ifndef LNL_SPAN_STAGE
-#define LNL_SPAN_STAGE 0  // 1: CRC mode stages the flushes' results and writes them in order per wave-batch
-#endif
-#ifndef LNL_SPAN_COUNT_STORES
-#define LNL_SPAN_COUNT_STORES 0  // 1: the row waits count the flushes' result stores (vmcnt(8 + e))
-#endif
 #ifndef LNL_SPAN_FIN_LDS
 #define LNL_SPAN_FIN_LDS 0  // 1: the heads' final map from the LDS tables (TB, TA), not the global FIN table
 #endif
@@ -126,27 +120,7 @@ enum : uint32_t { kTypeNormal = 0, kTypeHead = 1, kTypeTail = 2 };
 // A datagram's result: its CRC (kSpanCrc) or its LNL_INBOUND_* status from the
 // whole-datagram CRC.  (The timeline build, LNL_SPAN_DIAG & 16, stores none:
 // out[] carries its stamps.)
-#ifndef LNL_SPAN_STORE_POL
-#define LNL_SPAN_STORE_POL 0  // CRC result stores: 0 compiler's; 1 nt; 2 sc1; 3 sc0 sc1; 4 sc0 (experiments)
-#endif
 __device__ LNL_INLINE void store_result(const SpanArgs& A, uint32_t i, uint32_t crc, uint32_t len, uint32_t hdr) {
-#if LNL_SPAN_STORE_POL && !defined(LNL_SPAN_DIAG)
-    if (A.mode == kSpanCrc) {
-        const uint64_t a = (uint64_t)(uintptr_t)(A.out + i);
-#if LNL_SPAN_STORE_POL == 1
-        asm volatile("global_store_dword %0, %1, off nt" ::"v"(a), "v"(crc) : "memory");
-#elif LNL_SPAN_STORE_POL == 2
-        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(a), "v"(crc) : "memory");
-#elif LNL_SPAN_STORE_POL == 3
-        asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(a), "v"(crc) : "memory");
-#else
-        asm volatile("global_store_dword %0, %1, off sc0" ::"v"(a), "v"(crc) : "memory");
-#endif
-    } else {
-        A.ok[i] = (uint8_t)lnl_span_status(A.mode, crc, len, hdr);
-    }
-    return;
-#endif
 #if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 128)
     if (A.mode == kSpanCrc && crc == 0xFFFFFFFFu && len == 0xFFFFFFFFu) A.out[i] = hdr;  // diagnostic build only: (almost) no CRC stores
     else if (A.mode != kSpanCrc) A.ok[i] = (uint8_t)lnl_span_status(A.mode, crc, len, hdr);
@@ -250,33 +224,6 @@ __device__ LNL_INLINE void row_load(u32x4& v, uint64_t addr) {
 // counted vmcnt, so that the rows stay in flight meanwhile
 __device__ LNL_INLINE void off_load(uint64_t& v, uint64_t addr) {
     asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(addr) : "memory");
-}
-
-// Exactly one vector store instruction under lane mask m (m != 0), whatever
-// the exec mask around it: the row loop counts these in its vmcnt waits (a
-// store issued after a row's loads is younger than them, and an uncounted one
-// would make the next counted wait drain part of the following row too).
-__device__ LNL_INLINE void store_dword_always(uint64_t m, uint64_t addr, uint32_t v) {
-    uint64_t save;
-    asm volatile(
-        "s_mov_b64 %0, exec\n\t"
-        "s_mov_b64 exec, %1\n\t"
-        "global_store_dword %2, %3, off\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(save)
-        : "s"(m), "v"(addr), "v"(v)
-        : "memory");
-}
-__device__ LNL_INLINE void store_byte_always(uint64_t m, uint64_t addr, uint32_t v) {
-    uint64_t save;
-    asm volatile(
-        "s_mov_b64 %0, exec\n\t"
-        "s_mov_b64 exec, %1\n\t"
-        "global_store_byte %2, %3, off\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(save)
-        : "s"(m), "v"(addr), "v"(v)
-        : "memory");
 }
 
 // 16 bytes to LDS at addr + OFF (immediate offset)
@@ -850,21 +797,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 
         // ---- stash (wave-uniform counters) ---------------------------------
         uint32_t st_head = 0, st_tail = 0, head_slot = 0, tail_slot = 0;
-#if LNL_SPAN_STAGE
-        // CRC mode: the wave-batch's first datagram index, and the results
-        // staged so far (stage[kb + j]; kb + j stays inside [kb, k1 of lane 63))
-        const uint32_t kb = uni((uint32_t)__shfl((int)k0, 0, 64));
-        uint32_t nstaged = 0;
-        auto stage_result = [&](bool sr, uint32_t idx, uint32_t crc) {
-            const uint64_t m = __ballot(sr);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (sr) A.stage[kb + nstaged + rank] = make_uint2(idx, crc);
-            nstaged += (uint32_t)__popcll(m);
-        };
-#endif
-        // counted result stores (LNL_SPAN_COUNT_STORES): nst so far; mark_cur /
-        // mark_nxt, nst when the rows in flight (t, t + 1) were issued
-        uint32_t nst = 0, mark_cur = 0, mark_nxt = 0;
         uint32_t hpos = 0, tpos = 0, r_head = 0, r_tail = 0, hk = 0, hinfo = 0, tcs = 0, thdr = 0;
         bool hpend = false, tpend = false, htrack = false;
 
@@ -899,39 +831,9 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
 #else
             const uint32_t crc = final_crc_lds(tab_base, e, r);
 #endif
-#if LNL_SPAN_COUNT_STORES && !(defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & (16 | 128)))
-            {
-                // one store instruction per flush, always issued (lane 0 writes a
-                // spare control word when no entry is a whole datagram), and counted
-                const bool sr = act && type == kTypeNormal && mt.x < n;  // (the index check only guards the store)
-                uint64_t m = __ballot(sr);
-                const uint64_t junk = (uint64_t)(uintptr_t)(A.ctl + 7);
-                if (m == 0ull) m = 1ull;
-                if (A.mode == kSpanCrc) {
-                    store_dword_always(m, sr ? (uint64_t)(uintptr_t)(A.out + mt.x) : junk, crc);
-                } else {
-                    const uint32_t st = lnl_span_status(A.mode, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
-                    store_byte_always(m, sr ? (uint64_t)(uintptr_t)(A.ok + mt.x) : junk, st);
-                }
-                ++nst;
-            }
-#elif defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 256)
-            // diagnostic build only: the flush's results stored coalesced (one
-            // 256-byte run per flush into the overflow list's space; wrong results)
-            if (act && type == kTypeNormal && mt.x < n) {
-                A.ovf[((gw * 64u + (st_head >> 6)) * 64u + lane) % n] = crc ^ mt.x;
-            }
-#elif LNL_SPAN_STAGE
-            if (!WALK && A.mode == kSpanCrc) {
-                stage_result(act && type == kTypeNormal && mt.x < n, mt.x, crc);
-            } else if (act && type == kTypeNormal && mt.x < n) {
-                store_result(A, mt.x, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
-            }
-#else
             if (act && type == kTypeNormal && mt.x < n) {  // (the index check only guards the store)
                 store_result(A, mt.x, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
             }
-#endif
             // head / tail folds back to the lanes that own them
             const uint32_t hs = hpos - st_head, ts = tpos - st_head;
             const uint32_t rh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (hs & 63u)), (int)r);
@@ -1097,41 +999,12 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint32_t cnt = st_tail - st_head;
                 if (cnt >= (uint32_t)LNL_SPAN_EARLY_FLUSH) flush(cnt < kFlush ? cnt : kFlush, sin);
             }
-#if LNL_SPAN_COUNT_STORES
-            // younger than row t: row t + 1's 8 loads and the e counted stores
-            // issued since row t went out (at most 6 counted: waiting for more
-            // than needed is safe, for less is not)
-            if (t + 1u < R) {
-                const uint32_t e = uni(nst - mark_cur);
-                if (e == 0u)
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                else if (e == 1u)
-                    asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-                else if (e == 2u)
-                    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-                else if (e == 3u)
-                    asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
-                else if (e == 4u)
-                    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-                else if (e == 5u)
-                    asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            Transpose<0>::write(we, wo, cur);
-            if (t + 2u < R) issue(t + 2u, cur);
-            mark_cur = mark_nxt;
-            mark_nxt = nst;
-#else
             if (t + 1u < R)
                 asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             Transpose<0>::write(we, wo, cur);
             if (t + 2u < R) issue(t + 2u, cur);
-#endif
 #if LNL_SPAN_PRIO == 0
             // Issue fairness.  The two waves of a SIMD (wave, wave ^ 4) tie on
             // most issue slots, and ties go to the older wave: left alone, one
@@ -1276,11 +1149,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                 const uint32_t type = (mt.y >> 8) & 3u, e = mt.y & 127u;
                 uint32_t crc = 0u;
                 if (act) crc = final_crc_lds(tab_base, e, r);
-#if LNL_SPAN_STAGE
-                if (!WALK && A.mode == kSpanCrc)
-                    stage_result(act && type == kTypeNormal && mt.x < n, mt.x, crc);
-                else
-#endif
                 if (act && type == kTypeNormal && mt.x < n) store_result(A, mt.x, crc, mt.y >> 18, (mt.y >> 10) & 0xFFu);
                 const uint32_t hs = hpos - st_head;
                 const uint32_t rh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (hs & 63u)), (int)r);
@@ -1333,38 +1201,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_span_kernel(SpanArgs A) {
                     thdr = chdr;
                 }
                 tdone = true;
-            }
-        }
-#endif
-#if LNL_SPAN_STAGE
-        // CRC mode: the staged results in datagram order.  Slot p of the
-        // wave's row image (free now) takes datagram kb + p as {crc, index + 1}
-        // (0: none -- heads, empty and overflow datagrams are written
-        // elsewhere); then the wave writes out[kb ..] in order.  A wave-batch
-        // spanning more datagrams than the image holds stores them directly.
-        if (!WALK && A.mode == kSpanCrc && nstaged != 0u) {
-            const uint32_t kend = uni((uint32_t)__shfl((int)k1, 63, 64));
-            const uint32_t span = uni(kend - kb);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's staging stores are out)
-            if (span <= kImageBytes / 8u) {
-                uint2* const img = reinterpret_cast<uint2*>(lds + kImageOff + wave * kImageBytes);
-                for (uint32_t p = lane; p < span; p += 64u) img[p] = make_uint2(0u, 0u);
-                for (uint32_t j = lane; j < nstaged; j += 64u) {
-                    const uint2 e = A.stage[kb + j];
-                    img[e.x - kb] = make_uint2(e.y, e.x + 1u);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (uint32_t p = lane; p < span; p += 64u) {
-                    const uint2 v = img[p];
-                    if (v.y == kb + p + 1u) A.out[kb + p] = v.x;
-                }
-            } else {
-                for (uint32_t j = lane; j < nstaged; j += 64u) {
-                    const uint2 e = A.stage[kb + j];
-                    A.out[e.x] = e.y;
-                }
             }
         }
 #endif
@@ -1469,20 +1305,13 @@ size_t span_scratch_zero_words(uint32_t waves) {
     return 2 * kSpanCtlWords + (size_t)(span_max_segments(waves) / 64u) * kSpanXchWords;
 }
 
-size_t span_scratch_words(uint32_t n, uint32_t waves) {
-    return span_scratch_zero_words(waves) + n + (LNL_SPAN_STAGE ? 2u * (size_t)n + 2u : 0u);
-}
+size_t span_scratch_words(uint32_t n, uint32_t waves) { return span_scratch_zero_words(waves) + n; }
 
 void span_scratch_layout(SpanArgs& a, uint32_t* s, uint32_t parity) {
     a.ctl = s + kSpanCtlWords * (parity & 1u);
     a.ctl_next = s + kSpanCtlWords * (~parity & 1u);
     a.xch = s + 2 * kSpanCtlWords;
     a.ovf = s + span_scratch_zero_words(a.waves);
-    a.stage = nullptr;
-    if (LNL_SPAN_STAGE) {  // after the overflow list, 8-byte aligned (the scratch base is)
-        const size_t o = span_scratch_zero_words(a.waves) + a.n;
-        a.stage = reinterpret_cast<uint2*>(s + ((o + 1u) & ~(size_t)1));
-    }
 }
 
 hipError_t launch_span(const SpanArgs& a, int grid, hipStream_t stream) {

@@ -77,13 +77,7 @@ VARIANTS = {
     "span_noF": "-DLNL_SPAN_DIAG=4",                # CSR span kernel: boundaries without the F(b) read (wrong CRCs)
     "span_noput": "-DLNL_SPAN_DIAG=8",              # ... without the stash writes (wrong CRCs)
     # (span_pre2, a row's second boundary piece read with the first boundary's F(b): commit 1545e07, measured no gain, removed)
-    "span_cnt": "-DLNL_SPAN_COUNT_STORES=1",        # span kernel: row waits count the flushes' result stores
-    "span_coalst": "-DLNL_SPAN_DIAG=256",            # ... the flushes' results stored coalesced to scratch instead (wrong results)
-    "span_st_nt": "-DLNL_SPAN_STORE_POL=1",         # span kernel: CRC result stores nt / sc1 / sc0 sc1 / sc0
-    "span_st_sc1": "-DLNL_SPAN_STORE_POL=2",
-    "span_st_sc01": "-DLNL_SPAN_STORE_POL=3",
-    "span_st_sc0": "-DLNL_SPAN_STORE_POL=4",
-    "span_stage": "-DLNL_SPAN_STAGE=1",            # span kernel: CRC results staged, written in datagram order per wave-batch
+    # (span_cnt / span_st_* / span_stage / span_coalst: the result-store experiments of commit 9db95bb, removed)
     "span_nostore": "-DLNL_SPAN_DIAG=128",           # ... CRC mode without its result stores (wrong results)
     "span_nob2": "-DLNL_SPAN_DIAG=64",              # ... a row's second and later boundaries skipped (wrong CRCs)
     "bucketed": ("", 4),                            # CSR: the bucketed batch kernel (previous default)
