@@ -134,7 +134,10 @@ int lnl_inbound_filter_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uin
  * overlapped; lnl_crc32c_batch_host_ex below sets the count), writes
  * h_out[i], blocks until done.  h_off as in batch_csr_dev (h_off[0] may be
  * nonzero).  Pinned (hipHostMalloc / hipHostRegister) buffers give the full
- * PCIe rate; pageable ones work but copy through a staging buffer. */
+ * PCIe rate; pageable ones work but copy through a staging buffer.  (A
+ * pageable h_out -- CRCs here, statuses for lnl_inbound_filter_host, h_crc for
+ * lnl_crc32c_append_host -- goes through the library's own pinned staging,
+ * chunk by chunk, so it does not slow the pipeline.) */
 int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t n,
                           uint32_t* h_out, int device);
 
