@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LNL_CRC32C_ABI_VERSION 9
+#define LNL_CRC32C_ABI_VERSION 10
 
 /* Bytes the layer adds to every datagram (upstream ExtraPacketSizeForLayer). */
 #define LNL_CRC32C_LAYER_EXTRA 4
@@ -147,9 +147,11 @@ int lnl_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_off, uint32_t
  * it carries, cut as net_peer::process_packet does
  * (/root/reference/src/lnl/net_peer.cpp:164-187: [u16 LE size][packet]...,
  * stopping at the first packet net_packet::verify rejects or that runs past
- * the datagram).  Packet k: base[d_pkt_start[k] .. + d_pkt_len[k]) from
- * datagram d_pkt_parent[k], in datagram order.  *d_total (device) receives
- * the number of packets; only the first `cap` are written.  Stream-ordered. */
+ * the datagram; lnl_dispatch_csr_dev_ex below can walk as the reference's
+ * own buffer does instead).  Packet k: base[d_pkt_start[k] .. + d_pkt_len[k])
+ * from datagram d_pkt_parent[k], in datagram order.  *d_total (device)
+ * receives the number of packets; only the first `cap` are written.
+ * Stream-ordered. */
 int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, const uint8_t* d_status,
                          uint64_t* d_pkt_start, uint32_t* d_pkt_len, uint32_t* d_pkt_parent, uint32_t cap,
                          uint32_t* d_total, void* hip_stream);
@@ -164,6 +166,55 @@ int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d
                                         uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
                                         uint32_t* d_pkt_parent, uint32_t cap, uint32_t* d_total,
                                         void* hip_stream);
+
+/* Where the MERGED walk may read (lnl_dispatch_opts.tail).  The reference
+ * bounds its walk by the received packet's buffer capacity, not by the
+ * datagram (/root/reference/src/lnl/net_peer.cpp:167-183, buffer_size() at
+ * :171), and that buffer is always a fresh zero-filled 2048-byte one
+ * (net_packet() -> ensure(1432), include/lnl/net_packet.h:46-49, 194-208;
+ * pool_recycle deletes every buffer over MAX_PACKET_SIZE,
+ * src/lnl/net_manager.cpp:290-292).  So a size field in a container's last
+ * byte, or an entry that runs past the datagram, is cut from the bytes after
+ * it, and the reference delivers a zero-padded packet.
+ *   LNL_DISPATCH_TAIL_DATAGRAM  stop at the datagram's end (the default of
+ *                               lnl_dispatch_csr_dev; identical for every
+ *                               container net_peer::send_merged builds)
+ *   LNL_DISPATCH_TAIL_ZERO      the reference handed the stripped datagram:
+ *                               zeros right after it, the walk bounded by the
+ *                               2048-byte capacity
+ *   LNL_DISPATCH_TAIL_LAYER     the reference with INTEGRATION.md's
+ *                               receive_logic edit: the layer shrinks the
+ *                               packet, so the 4 stripped CRC bytes stay in
+ *                               the buffer after it, then zeros
+ * Under the two tail rules a packet may extend past the bytes its datagram
+ * holds: d_pkt_len[k] is the reference's length, d_pkt_avail[k] (optional)
+ * how many of its bytes, from d_pkt_start[k], are the wire burst's (the
+ * datagram, or the datagram and its CRC field); the caller zero-fills the
+ * remaining d_pkt_len[k] - d_pkt_avail[k].  (Under the datagram rule
+ * d_pkt_avail[k] == d_pkt_len[k].)  A nested container is one packet under
+ * every rule: the caller's process_packet cuts it again (with a zero tail, as
+ * the reference's fresh pool packet has). */
+#define LNL_DISPATCH_TAIL_DATAGRAM 0
+#define LNL_DISPATCH_TAIL_ZERO 1
+#define LNL_DISPATCH_TAIL_LAYER 2
+typedef struct lnl_dispatch_opts {
+    uint32_t size;        /* sizeof(lnl_dispatch_opts) */
+    uint32_t tail;        /* LNL_DISPATCH_TAIL_* */
+    uint32_t reserved[2]; /* 0 */
+} lnl_dispatch_opts;
+
+/* lnl_dispatch_csr_dev / lnl_inbound_filter_dispatch_csr_dev with options
+ * (opts NULL: the datagram rule) and the per-packet in-burst byte counts
+ * (d_pkt_avail, cap entries, may be NULL).  -EINVAL for a bad size, tail or
+ * reserved field. */
+int lnl_dispatch_csr_dev_ex(const uint8_t* d_base, const uint64_t* d_off, uint32_t n, const uint8_t* d_status,
+                            uint64_t* d_pkt_start, uint32_t* d_pkt_len, uint32_t* d_pkt_parent,
+                            uint32_t* d_pkt_avail, uint32_t cap, uint32_t* d_total, const lnl_dispatch_opts* opts,
+                            void* hip_stream);
+int lnl_inbound_filter_dispatch_csr_dev_ex(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                           uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
+                                           uint32_t* d_pkt_parent, uint32_t* d_pkt_avail, uint32_t cap,
+                                           uint32_t* d_total, const lnl_dispatch_opts* opts, void* hip_stream);
 
 /* Upstream LiteNetLib's XOR-encryption layer (XorEncryptLayer; SURVEY.md 8(f)
  * item 4), in place: data[i] ^= key[i % key_len] for i < length, the key phase

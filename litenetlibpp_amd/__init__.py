@@ -15,6 +15,9 @@ from .crc32c import (  # noqa: F401
     batch_host,
     batch_host_multi,
     dispatch,
+    DISPATCH_TAIL_DATAGRAM,
+    DISPATCH_TAIL_LAYER,
+    DISPATCH_TAIL_ZERO,
     egress_send_batch,
     filter_dispatch,
     xor_layer,

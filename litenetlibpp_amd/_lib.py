@@ -34,6 +34,17 @@ class HostOpts(ctypes.Structure):
         return cls(ctypes.sizeof(cls), streams, chunk_datagrams, 0, chunk_bytes)
 
 
+class DispatchOpts(ctypes.Structure):
+    """struct lnl_dispatch_opts (include/lnl_crc32c.h)."""
+    _fields_ = [("size", ctypes.c_uint32), ("tail", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 2)]
+
+    @classmethod
+    def make(cls, tail: int = 0) -> "DispatchOpts":
+        return cls(ctypes.sizeof(cls), tail)
+
+
+DISPATCH_TAIL_DATAGRAM, DISPATCH_TAIL_ZERO, DISPATCH_TAIL_LAYER = 0, 1, 2  # LNL_DISPATCH_TAIL_*
+
 HOST_MAX_STREAMS = 8       # LNL_HOST_MAX_STREAMS
 HOST_DEFAULT_STREAMS = 4   # LNL_HOST_DEFAULT_STREAMS
 
@@ -95,6 +106,14 @@ def lib() -> ctypes.CDLL:
     L.lnl_inbound_filter_dispatch_csr_dev.restype = ctypes.c_int
     L.lnl_inbound_filter_dispatch_csr_dev.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, _c_u8p,
                                                       _c_u8p, ctypes.c_uint32, _c_u8p, ctypes.c_void_p]
+    dopts_p = ctypes.POINTER(DispatchOpts)
+    L.lnl_dispatch_csr_dev_ex.restype = ctypes.c_int
+    L.lnl_dispatch_csr_dev_ex.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, _c_u8p, _c_u8p, _c_u8p,
+                                          ctypes.c_uint32, _c_u8p, dopts_p, ctypes.c_void_p]
+    L.lnl_inbound_filter_dispatch_csr_dev_ex.restype = ctypes.c_int
+    L.lnl_inbound_filter_dispatch_csr_dev_ex.argtypes = [_c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, _c_u8p, _c_u8p,
+                                                         _c_u8p, _c_u8p, ctypes.c_uint32, _c_u8p, dopts_p,
+                                                         ctypes.c_void_p]
     L.lnl_xor_layer.restype = ctypes.c_int
     L.lnl_xor_layer.argtypes = [_c_u8p, ctypes.c_size_t, _c_u8p, ctypes.c_size_t]
     L.lnl_xor_layer_csr_dev.restype = ctypes.c_int

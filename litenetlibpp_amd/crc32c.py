@@ -26,7 +26,8 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import HOST_DEFAULT_STREAMS, HOST_MAX_STREAMS, Crc32cError, HostOpts, check, lib
+from ._lib import (DISPATCH_TAIL_DATAGRAM, DISPATCH_TAIL_LAYER, DISPATCH_TAIL_ZERO, HOST_DEFAULT_STREAMS,
+                   HOST_MAX_STREAMS, Crc32cError, DispatchOpts, HostOpts, check, lib)
 
 EXTRA_PACKET_SIZE = 4  # LNL_CRC32C_LAYER_EXTRA / upstream ExtraPacketSizeForLayer
 HEADER_SIZE = 1        # net_constants::HEADER_SIZE (/root/reference/include/lnl/net_constants.h:16)
@@ -35,7 +36,7 @@ __all__ = [
     "Crc32cError", "EXTRA_PACKET_SIZE", "crc32c", "crc32c_extend", "Crc32cLayer",
     "batch_fixed", "batch_csr", "verify_csr", "batch_host", "batch_host_multi", "mtu_with_layer",
     "packet_verify", "inbound_status", "inbound_filter", "filter_dispatch", "inbound_filter_host", "ingress_recv_batch",
-    "dispatch", "xor_layer", "xor_layer_csr", "xor_layer_fixed",
+    "dispatch", "DISPATCH_TAIL_DATAGRAM", "DISPATCH_TAIL_ZERO", "DISPATCH_TAIL_LAYER", "xor_layer", "xor_layer_csr", "xor_layer_fixed",
     "INGRESS_SLOT", "HOST_DEFAULT_STREAMS", "HOST_MAX_STREAMS", "stream_release",
     "INBOUND_DROP_CRC", "INBOUND_ACCEPT", "INBOUND_MALFORMED",
 ]
@@ -242,11 +243,22 @@ def inbound_filter(data, offsets, out=None, stream=None):
     return status
 
 
-def dispatch(data, offsets, status, cap: Optional[int] = None, stream=None):
+def _dispatch_opts(tail: int):
+    if tail not in (DISPATCH_TAIL_DATAGRAM, DISPATCH_TAIL_ZERO, DISPATCH_TAIL_LAYER):
+        raise ValueError(f"tail must be one of DISPATCH_TAIL_* (0, 1, 2), got {tail}")
+    return ctypes.byref(DispatchOpts.make(tail))
+
+
+def dispatch(data, offsets, status, cap: Optional[int] = None, stream=None, tail: int = DISPATCH_TAIL_DATAGRAM,
+             avail: bool = False):
     """Packets a filtered burst delivers, on the GPU: accepted datagrams (CRC
-    stripped) and the packets of MERGED containers.  Returns (start int64,
-    length int32, parent int32) tensors of the delivered packets (all of them
-    when cap is None: a first call counts, a second fills)."""
+    stripped) and the packets of MERGED containers (lnl_dispatch_csr_dev_ex).
+    Returns (start int64, length int32, parent int32) tensors of the delivered
+    packets (all of them when cap is None: a first call counts, a second
+    fills), plus the in-burst byte counts (int32) when avail is set.  tail:
+    the walk's bound past the datagram (DISPATCH_TAIL_DATAGRAM: stop there;
+    DISPATCH_TAIL_ZERO / DISPATCH_TAIL_LAYER: the reference's zero-filled
+    2048-byte buffer, net_peer.cpp:167-183; see include/lnl_crc32c.h)."""
     torch = _torch()
     _check_dev_u8(data, "data")
     _check_off(offsets, data)
@@ -255,30 +267,37 @@ def dispatch(data, offsets, status, cap: Optional[int] = None, stream=None):
     if not (isinstance(status, torch.Tensor) and status.is_cuda and status.dtype == torch.uint8
             and status.is_contiguous() and status.numel() >= max(n, 0) and status.device == dev):
         raise TypeError("status must be a contiguous uint8 CUDA tensor of >= n entries on the data's device")
+    opts = _dispatch_opts(tail)
     total = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def run(c):
         start = torch.empty(max(c, 1), dtype=torch.int64, device=dev)
         length = torch.empty(max(c, 1), dtype=torch.int32, device=dev)
         parent = torch.empty(max(c, 1), dtype=torch.int32, device=dev)
-        check(lib().lnl_dispatch_csr_dev(data.data_ptr(), offsets.data_ptr(), max(n, 0), status.data_ptr(),
-                                         start.data_ptr(), length.data_ptr(), parent.data_ptr(), c,
-                                         total.data_ptr(), _stream_handle(stream)), "lnl_dispatch_csr_dev")
-        return start, length, parent
+        av = torch.empty(max(c, 1), dtype=torch.int32, device=dev) if avail else None
+        check(lib().lnl_dispatch_csr_dev_ex(data.data_ptr(), offsets.data_ptr(), max(n, 0), status.data_ptr(),
+                                            start.data_ptr(), length.data_ptr(), parent.data_ptr(),
+                                            av.data_ptr() if avail else None, c, total.data_ptr(), opts,
+                                            _stream_handle(stream)), "lnl_dispatch_csr_dev_ex")
+        return start, length, parent, av
 
-    start, length, parent = run(cap if cap is not None else 0)
+    start, length, parent, av = run(cap if cap is not None else 0)
     t = int(total.item()) & 0xFFFFFFFF  # u32 count
     if cap is None:
-        start, length, parent = run(t)
+        start, length, parent, av = run(t)
         cap = t
     k = min(t, cap)
+    if avail:
+        return start[:k], length[:k], parent[:k], av[:k]
     return start[:k], length[:k], parent[:k]
 
 
-def filter_dispatch(data, offsets, cap: Optional[int] = None, out=None, stream=None):
+def filter_dispatch(data, offsets, cap: Optional[int] = None, out=None, stream=None,
+                    tail: int = DISPATCH_TAIL_DATAGRAM, avail: bool = False):
     """inbound_filter + dispatch in one pass over the bytes
-    (lnl_inbound_filter_dispatch_csr_dev).  Returns (status uint8, start int64,
-    length int32, parent int32); the packets as dispatch() returns them."""
+    (lnl_inbound_filter_dispatch_csr_dev_ex).  Returns (status uint8, start
+    int64, length int32, parent int32[, avail int32]); the packets as dispatch()
+    returns them."""
     torch = _torch()
     _check_dev_u8(data, "data")
     _check_off(offsets, data)
@@ -288,24 +307,28 @@ def filter_dispatch(data, offsets, cap: Optional[int] = None, out=None, stream=N
     if status.dtype != torch.uint8 or status.numel() < max(n, 0) or status.device != dev \
             or not status.is_contiguous():
         raise ValueError("out must be a contiguous uint8 tensor of n entries on the data's device")
+    opts = _dispatch_opts(tail)
     total = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def run(c):
         start = torch.empty(max(c, 1), dtype=torch.int64, device=dev)
         length = torch.empty(max(c, 1), dtype=torch.int32, device=dev)
         parent = torch.empty(max(c, 1), dtype=torch.int32, device=dev)
-        check(lib().lnl_inbound_filter_dispatch_csr_dev(
+        av = torch.empty(max(c, 1), dtype=torch.int32, device=dev) if avail else None
+        check(lib().lnl_inbound_filter_dispatch_csr_dev_ex(
             data.data_ptr(), offsets.data_ptr(), max(n, 0), status.data_ptr(), start.data_ptr(),
-            length.data_ptr(), parent.data_ptr(), c, total.data_ptr(), _stream_handle(stream)),
-            "lnl_inbound_filter_dispatch_csr_dev")
-        return start, length, parent
+            length.data_ptr(), parent.data_ptr(), av.data_ptr() if avail else None, c, total.data_ptr(), opts,
+            _stream_handle(stream)), "lnl_inbound_filter_dispatch_csr_dev_ex")
+        return start, length, parent, av
 
-    start, length, parent = run(cap if cap is not None else 0)
+    start, length, parent, av = run(cap if cap is not None else 0)
     t = int(total.item()) & 0xFFFFFFFF  # u32 count
     if cap is None:
-        start, length, parent = run(t)
+        start, length, parent, av = run(t)
         cap = t
     k = min(t, cap)
+    if avail:
+        return status, start[:k], length[:k], parent[:k], av[:k]
     return status, start[:k], length[:k], parent[:k]
 
 

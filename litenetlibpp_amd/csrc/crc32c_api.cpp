@@ -876,9 +876,34 @@ extern "C" int lnl_crc32c_append_host_ex(const uint8_t* h_payload, const uint64_
     return host_batch(h_payload, h_off, n, h_wire, device, kHostAppend, h_crc, opts);
 }
 
+namespace {
+// lnl_dispatch_opts -> DispatchArgs::tail (NULL: the datagram rule)
+int dispatch_tail(const lnl_dispatch_opts* o, uint32_t* tail) {
+    *tail = lnl::kDispatchTailDatagram;
+    if (!o) return 0;
+    if (o->size < sizeof(lnl_dispatch_opts)) return fail(-EINVAL, "lnl_dispatch_opts.size %u", o->size);
+    if (o->reserved[0] || o->reserved[1]) return fail(-EINVAL, "lnl_dispatch_opts.reserved must be 0");
+    if (o->tail > LNL_DISPATCH_TAIL_LAYER) return fail(-EINVAL, "lnl_dispatch_opts.tail %u", o->tail);
+    static_assert(LNL_DISPATCH_TAIL_ZERO == lnl::kDispatchTailZero && LNL_DISPATCH_TAIL_LAYER == lnl::kDispatchTailLayer,
+                  "tail modes");
+    *tail = o->tail;
+    return 0;
+}
+}  // namespace
+
 extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
                                     const uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
                                     uint32_t* d_pkt_parent, uint32_t cap, uint32_t* d_total, void* hip_stream) {
+    return lnl_dispatch_csr_dev_ex(d_base, d_off, n, d_status, d_pkt_start, d_pkt_len, d_pkt_parent, nullptr, cap,
+                                   d_total, nullptr, hip_stream);
+}
+
+extern "C" int lnl_dispatch_csr_dev_ex(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                       const uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
+                                       uint32_t* d_pkt_parent, uint32_t* d_pkt_avail, uint32_t cap,
+                                       uint32_t* d_total, const lnl_dispatch_opts* opts, void* hip_stream) {
+    uint32_t tail = 0;
+    if (int rc = dispatch_tail(opts, &tail)) return rc;
     if (!d_total) return fail(-EINVAL, "d_total is NULL");
     hipStream_t st = (hipStream_t)hip_stream;
     if (n == 0) {
@@ -904,7 +929,7 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     constexpr bool onepass = false;   // product: count + scan + emit
     constexpr uint32_t nt_stores = 0;  // plain stores (nt measured neutral)
 #endif
-    if (onepass) {
+    if (onepass && !tail && !d_pkt_avail) {
         const size_t nwg = ((size_t)n + 255) / 256;
         void* flags = nullptr;
         hipError_t e = hipMallocAsync(&flags, nwg * 8, st);
@@ -951,6 +976,8 @@ extern "C" int lnl_dispatch_csr_dev(const uint8_t* d_base, const uint64_t* d_off
     a.pkt_start = d_pkt_start;
     a.pkt_len = d_pkt_len;
     a.pkt_parent = d_pkt_parent;
+    a.pkt_avail = cap ? d_pkt_avail : nullptr;
+    a.tail = tail;
     a.cap = cap;
     a.total = d_total;
     void* tmp = (void*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);
@@ -970,6 +997,17 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
                                                    uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
                                                    uint32_t* d_pkt_parent, uint32_t cap, uint32_t* d_total,
                                                    void* hip_stream) {
+    return lnl_inbound_filter_dispatch_csr_dev_ex(d_base, d_off, n, d_status, d_pkt_start, d_pkt_len, d_pkt_parent,
+                                                  nullptr, cap, d_total, nullptr, hip_stream);
+}
+
+extern "C" int lnl_inbound_filter_dispatch_csr_dev_ex(const uint8_t* d_base, const uint64_t* d_off, uint32_t n,
+                                                      uint8_t* d_status, uint64_t* d_pkt_start, uint32_t* d_pkt_len,
+                                                      uint32_t* d_pkt_parent, uint32_t* d_pkt_avail, uint32_t cap,
+                                                      uint32_t* d_total, const lnl_dispatch_opts* opts,
+                                                      void* hip_stream) {
+    uint32_t tail = 0;
+    if (int rc = dispatch_tail(opts, &tail)) return rc;
     if (!d_total) return fail(-EINVAL, "d_total is NULL");
     hipStream_t st = (hipStream_t)hip_stream;
     if (n == 0) {
@@ -983,8 +1021,8 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     // (the span kernel indexes walk blocks as 8 k in 32 bits)
     if (n < LNL_BUCKET_MIN_N || n > (1u << 28) || csr_path() != kPathBucketed) {
         if (int rc = lnl_inbound_filter_csr_dev(d_base, d_off, n, d_status, hip_stream)) return rc;
-        return lnl_dispatch_csr_dev(d_base, d_off, n, d_status, d_pkt_start, d_pkt_len, d_pkt_parent, cap, d_total,
-                                    hip_stream);
+        return lnl_dispatch_csr_dev_ex(d_base, d_off, n, d_status, d_pkt_start, d_pkt_len, d_pkt_parent, d_pkt_avail,
+                                       cap, d_total, opts, hip_stream);
     }
     const uint32_t nwg = (uint32_t)(((size_t)n + 255) / 256);
     const bool prefix = nwg <= lnl::kDispatchPrefixWgs && !LNL_DISPATCH_SCAN;
@@ -1005,6 +1043,8 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev(const uint8_t* d_base, const 
     a.pkt_start = d_pkt_start;
     a.pkt_len = d_pkt_len;
     a.pkt_parent = d_pkt_parent;
+    a.pkt_avail = cap ? d_pkt_avail : nullptr;
+    a.tail = tail;
     a.cap = cap;
     a.total = d_total;
     uint32_t* blk = (uint32_t*)(((uintptr_t)(a.rec + (size_t)lnl::kDispatchRec * n) + 255) & ~(uintptr_t)255);

@@ -205,7 +205,22 @@ struct DispatchArgs {
     // here and the emit pass sums its predecessors' (no scan launch; first is
     // unused).  Null: the hipCUB scan of counts into first.
     uint32_t* wgsum;
+    // the walk's bound past the datagram (lnl_dispatch_opts.tail, lnl_dispatch.hip):
+    // kDispatchTailDatagram stops at it; the other two walk the reference's
+    // zero-filled buffer, and pkt_avail (cap, optional) receives the bytes of
+    // each packet that lie inside the datagram
+    uint32_t tail;
+    uint32_t* pkt_avail;
 };
+constexpr uint32_t kDispatchTailDatagram = 0, kDispatchTailZero = 1, kDispatchTailLayer = 2;
+// buffer_size() of the reference's received packet for a wire datagram of
+// `wire` bytes: net_packet() allocates 2048 (ensure(1432), net_packet.h:46-49,
+// 194-208) and resize() doubles it while it is short
+__host__ __device__ inline uint32_t dispatch_ref_capacity(uint32_t wire) {
+    uint32_t cap = 2048u;
+    while (cap < wire) cap *= 2u;
+    return cap;
+}
 constexpr uint32_t kDispatchPrefixWgs = 8192;
 constexpr uint32_t kDispatchRec = 8;  // packets per datagram kept from the counting walk
 constexpr uint32_t kWalkBlock = 8;             // fused path: words per datagram block [count, 7 records]

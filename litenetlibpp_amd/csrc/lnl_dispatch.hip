@@ -16,11 +16,26 @@
 //       if !verify(packet[pos .. pos+L)): stop         (L = 0 fails: no header byte)
 //       emit [pos, pos+L); pos += L
 //
-// (*) The reference bounds both reads by its pooled buffer's capacity
-// (buffer_size(), 2048 for received packets), not by the datagram, and reads
-// stale pool bytes past the datagram's end; a container that runs past its
-// datagram stops here instead.  Well-formed containers -- all send_merged
-// produces -- split identically.
+// (*) The default rule (LNL_DISPATCH_TAIL_DATAGRAM).  The reference bounds
+// its walk by the pooled buffer's capacity instead (net_peer.cpp:171,
+// buffer_size()), and that buffer is deterministic: every received packet is
+// a fresh net_packet() -- ensure(1432) zero-fills 2048 bytes
+// (net_packet.h:46-49, 194-208) -- because pool_recycle deletes any packet
+// whose buffer exceeds MAX_PACKET_SIZE (net_manager.cpp:290-292), which is
+// every one.  So past the datagram it reads zeros (or, with the layer's
+// receive_logic edit of INTEGRATION.md, the 4 stripped CRC bytes and then
+// zeros) and delivers zero-padded packets.  The tail modes reproduce that:
+//
+//   pos = 1
+//   while pos < size:
+//       L = u16 at pos (tail bytes past the datagram); pos += 2
+//       if cap - pos < L: stop                        (cap = 2048)
+//       if !verify(tail byte at pos, L): stop
+//       emit [pos, pos+L) with avail = the bytes of it inside the datagram
+//       (+ the CRC field, LNL_DISPATCH_TAIL_LAYER); pos += L
+//
+// Well-formed containers -- all send_merged produces -- split identically
+// under every rule.
 //
 // A nested container is delivered as one packet (the reference's
 // process_packet would cut it again); send_merged never nests.
@@ -64,6 +79,19 @@ __device__ inline uint32_t load3(const uint8_t* q) {
     return (uint32_t)(v >> ((a & 3u) * 8u));
 }
 
+// Bytes pos .. pos + 2 of a datagram of `size` bytes (CRC stripped) under a
+// tail rule: the datagram's own bytes below lim (size, or size + 4 with the
+// CRC field), zeros from there on.  Only the first byte of each lies past
+// the wire datagram: byte loads, so nothing outside the batch is touched.
+__device__ inline uint32_t tail_load3(const uint8_t* p, uint32_t pos, uint32_t size, uint32_t lim) {
+    if (pos + 3u <= size) return load3(p + pos);
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 3u; ++j)
+        if (pos + j < lim) v |= (uint32_t)p[pos + j] << (8u * j);
+    return v;
+}
+
 // Walk datagram i; for each delivered packet call emit(start, len) (start
 // relative to the datagram).  Returns the number of packets.
 template <typename F>
@@ -76,6 +104,21 @@ __device__ inline uint32_t walk(const DispatchArgs& a, uint64_t s, uint32_t size
         return 1;
     }
     uint32_t pos = 1, c = 0;
+    if (a.tail) {  // the reference's buffer: capacity-bounded, tail bytes past the datagram
+        const uint32_t lim = size + (a.tail == kDispatchTailLayer ? 4u : 0u);
+        const uint32_t cap = dispatch_ref_capacity(size + 4u);
+        while (pos < size) {
+            v = tail_load3(p, pos, size, lim);
+            const uint32_t L = v & 0xFFFFu;
+            pos += 2;
+            if (cap - pos < L) break;
+            if (L == 0u || !lnl_packet_verify_hdr((uint8_t)(v >> 16), L)) break;
+            emit(pos, L);
+            pos += L;
+            ++c;
+        }
+        return c;
+    }
     while (pos < size) {
         if (pos + 2u > size) break;
         if (pos != 1u) v = load3(p + pos);
@@ -145,16 +188,31 @@ __global__ __launch_bounds__(256) void dispatch_fix_kernel(DispatchArgs a) {
         const uint4* blk = reinterpret_cast<const uint4*>(a.blk + (size_t)i * kWalkBlock);
         const uint4 b0 = walked ? blk[0] : make_uint4(kWalkBlock, 0u, 0u, 0u);
         c = b0.x;
+        bool again = c >= kWalkBlock && c != kWalkPlain;
         if (c == kWalkPlain) {  // the datagram itself, CRC stripped
             a.rec[i] = (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
             c = 1;
         } else if (c < kWalkBlock) {
             const uint4 b1 = blk[1];
             const uint32_t r[7] = {b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            // the span kernel walks by the datagram rule; under a tail rule a
+            // container it stopped short of its end may read on past it, so
+            // that one is walked again here (well-formed ones end exactly)
+            if (a.tail) {
+                uint32_t last = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < 7; ++k)
-                if (k < c) a.rec[(size_t)k * a.n + i] = r[k];
-        } else {
+                for (uint32_t k = 0; k < 7; ++k)
+                    if (k + 1u == c) last = r[k];
+                const uint32_t next = c ? (last >> 16) + (last & 0xFFFFu) : 1u;
+                again = next < (uint32_t)(a.off[i + 1] - a.off[i]) - 4u;
+            }
+            if (!again) {
+#pragma unroll
+                for (uint32_t k = 0; k < 7; ++k)
+                    if (k < c) a.rec[(size_t)k * a.n + i] = r[k];
+            }
+        }
+        if (again) {
             const uint64_t o0 = a.off[i], o1 = a.off[i + 1];
             const uint32_t size = (uint32_t)(o1 - o0) - 4u;
             uint32_t k = 0;
@@ -180,9 +238,16 @@ __global__ __launch_bounds__(256) void dispatch_fix_kernel(DispatchArgs a) {
 // Longer containers are walked again by their own lane.
 constexpr uint32_t kEmitMaxSteps = 16;  // cooperative only while the range is <= 16 x 64 packets
 
+// packet bytes [pos, pos + len) of a datagram whose own bytes end at lim
+__device__ inline uint32_t pkt_avail(uint32_t pos, uint32_t len, uint32_t lim) {
+    const uint32_t in = lim > pos ? lim - pos : 0u;
+    return in < len ? in : len;
+}
+
 __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
     __shared__ uint32_t s_first[4][65];
     __shared__ uint32_t s_fast[4][64];
+    __shared__ uint32_t s_lim[4][64];
     __shared__ uint64_t s_start[4][64];
     __shared__ uint32_t s_rec[4][kDispatchRec][64];
     __shared__ uint32_t s_part[4], s_wsum[4];
@@ -226,11 +291,17 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
     } else if (i0 < a.n) {
         f = a.first[a.n - 1] + a.counts[a.n - 1];  // past the end: empty, first = total
     }
-    const bool fast = c <= kDispatchRec && size < 65536u;
+    // (positions are 16-bit in the records: a tail walk's reach past its
+    // datagram stays below size + 2)
+    const bool fast = c <= kDispatchRec && size < 65534u;
+    // bytes of the datagram a packet may take as its own: the rest of a
+    // packet cut under a tail rule is the caller's zero fill (pkt_avail)
+    const uint32_t lim = a.tail ? size + (a.tail == kDispatchTailLayer ? 4u : 0u) : 0xFFFFFFFFu;
     s_first[w][lane] = f;
     if (lane == 63u) s_first[w][64] = f + c;
     s_fast[w][lane] = fast;
     s_start[w][lane] = s;
+    s_lim[w][lane] = lim;
     for (uint32_t k = 0; k < kDispatchRec; ++k)
         if (fast && k < c) s_rec[w][k][lane] = a.rec[(size_t)k * a.n + i];
     __syncthreads();
@@ -254,6 +325,7 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
                 a.pkt_len[j] = r & 0xFFFFu;
                 a.pkt_parent[j] = i0 + lo;
             }
+            if (a.pkt_avail) a.pkt_avail[j] = pkt_avail(r >> 16, r & 0xFFFFu, s_lim[w][lo]);
         }
     }
     if (c == 0u || f >= a.cap || (coop && fast)) return;
@@ -262,6 +334,7 @@ __global__ __launch_bounds__(256) void dispatch_emit_kernel(DispatchArgs a) {
             a.pkt_start[f + k] = s + pos;
             a.pkt_len[f + k] = len;
             a.pkt_parent[f + k] = i;
+            if (a.pkt_avail) a.pkt_avail[f + k] = pkt_avail(pos, len, lim);
         }
     };
     if (fast) {
@@ -440,7 +513,8 @@ hipError_t launch_dispatch(const DispatchArgs& a, void* scan_tmp, size_t scan_by
     const dim3 grid((a.n + 255u) / 256u);
     if (a.wgsum && grid.x > kDispatchPrefixWgs) return hipErrorInvalidValue;
 #if LNL_EXPERIMENTS
-    if (a.look) {  // one pass (flags zeroed by the caller)
+    if (a.look) {  // one pass (flags zeroed by the caller; the datagram rule only)
+        if (a.tail || a.pkt_avail) return hipErrorInvalidValue;
         hipLaunchKernelGGL(dispatch_onepass_kernel, grid, dim3(256), 0, stream, a);
         return hipGetLastError();
     }

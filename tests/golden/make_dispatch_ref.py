@@ -29,8 +29,18 @@ those containers only the first "agree" deliveries are common; ref_cut() below
 restates the reference's rules INCLUDING the zero tail, and this script checks it
 against what the reference actually delivered before writing anything.
 
+The same containers also go through the reference with the layer compiled in
+as INTEGRATION.md 2 writes it (variant crc_src: the injected datagram carries
+its CRC, receive_logic strips it by shrinking the packet).  The 4 CRC bytes
+then stay in the buffer right after the datagram, and the reference cuts them
+before the zeros:
+
+  tests/golden/dispatch_ref_layer.json   the same records for that variant
+
+ref_cut(..., tail=LE32(crc)) restates that and is checked the same way.
+
 Run in the build container (needs /root/reference and g++):
-    python3 oracle/refnet/build.py plain && python3 tests/golden/make_dispatch_ref.py
+    python3 oracle/refnet/build.py plain crc_src && python3 tests/golden/make_dispatch_ref.py
 """
 import json
 import os
@@ -44,6 +54,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 DRIVER = os.path.join(ROOT, "oracle", "_ref", "net", "plain", "refnet_driver")
+DRIVER_LAYER = os.path.join(ROOT, "oracle", "_ref", "net", "crc_src", "refnet_driver")
 
 MERGED, UNRELIABLE = 0x0C, 0x00
 CAP = 2048  # buffer_size() of every pooled packet (net_packet(): ensure(1432) -> 2048)
@@ -58,12 +69,13 @@ def verify(b0, size):
     return size >= hs and (not (b0 & 0x80) or size >= hs + 6)
 
 
-def ref_cut(pkt, conn, past=False):
+def ref_cut(pkt, conn, past=False, tail=b""):
     """process_packet (net_peer.cpp:138-243) on pkt for the cases crafted here:
     the connection-number check (:156), MERGED (:164-187, walk bounded by the
-    zero-filled 2048-byte buffer), UNRELIABLE (:240, deliver pkt[1:]).  Returns
-    [(payload, past)]: past = produced after a read beyond pkt's own bytes."""
-    buf = bytes(pkt) + bytes(CAP - len(pkt))
+    zero-filled 2048-byte buffer, whose bytes after pkt are `tail` and then
+    zeros), UNRELIABLE (:240, deliver pkt[1:]).  Returns [(payload, past)]:
+    past = produced after a read beyond pkt's own bytes."""
+    buf = bytes(pkt) + bytes(tail) + bytes(CAP - len(pkt) - len(tail))
     if ((buf[0] & 0x60) >> 5) != conn:
         return []
     prop = buf[0] & 0x1F
@@ -143,40 +155,55 @@ def build_containers(conn, seed=2024):
     return out
 
 
-def main():
-    if not os.path.exists(DRIVER):
-        sys.exit(f"{DRIVER} missing: python3 oracle/refnet/build.py plain")
-    conn = 0  # a manager's first connection (net_manager.cpp:984 counts up from there)
-    cont = build_containers(conn)
-    blob = b"LNLM" + struct.pack("<II", len(cont), conn) + b"".join(struct.pack("<I", len(c)) + c for c in cont)
+def run_driver(driver, blob):
     with tempfile.TemporaryDirectory() as td:
         fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.json")
         with open(fin, "wb") as f:
             f.write(blob)
-        r = subprocess.run([DRIVER, "merged", fin, fout], capture_output=True, text=True, timeout=600)
+        r = subprocess.run([driver, "merged", fin, fout], capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             sys.exit(f"driver failed: {r.stdout}\n{r.stderr}")
         with open(fout) as f:
-            res = json.load(f)
+            return json.load(f)
+
+
+def records_for(cont, conn, res, tails):
     assert res["containers"] == len(cont) and len(res["delivered"]) == len(cont)
     records, divergent = [], 0
-    for i, (c, got) in enumerate(zip(cont, res["delivered"])):
+    for i, (c, got, tail) in enumerate(zip(cont, res["delivered"], tails)):
         assert all(m == 4 for m, _ in got), (i, got)  # DELIVERY_METHOD::UNRELIABLE (net_enums.h)
         observed = [bytes.fromhex(p) for _, p in got]
-        model = ref_cut(c, conn)
+        model = ref_cut(c, conn, tail=tail)
         assert observed == [p for p, _ in model], (i, c.hex(), observed, model)
         agree = next((k for k, (_, past) in enumerate(model) if past), len(model))
         reads_past = any(past for _, past in model) or _reads_past(c, conn)
         divergent += reads_past
         records.append({"delivered": [p.hex() for p in observed], "agree": agree, "reads_past_datagram": reads_past})
+    return records, divergent
+
+
+def main():
+    for d, v in ((DRIVER, "plain"), (DRIVER_LAYER, "crc_src")):
+        if not os.path.exists(d):
+            sys.exit(f"{d} missing: python3 oracle/refnet/build.py {v}")
+    sys.path.insert(0, os.path.dirname(HERE))
+    import oracle  # the CPU CRC-32C (test infrastructure): the layer's field
+    conn = 0  # a manager's first connection (net_manager.cpp:984 counts up from there)
+    cont = build_containers(conn)
+    blob = b"LNLM" + struct.pack("<II", len(cont), conn) + b"".join(struct.pack("<I", len(c)) + c for c in cont)
+    src = ("oracle/_ref/net/{}/refnet_driver merged (the reference's net_peer::process_packet, "
+           "net_peer.cpp:164-187), tests/golden/make_dispatch_ref.py")
+    for name, driver, variant, tails in (
+            ("dispatch_ref.json", DRIVER, "plain", [b""] * len(cont)),
+            ("dispatch_ref_layer.json", DRIVER_LAYER, "crc_src",
+             [struct.pack("<I", oracle.crc(np.frombuffer(c, np.uint8))) for c in cont])):
+        records, divergent = records_for(cont, conn, run_driver(driver, blob), tails)
+        with open(os.path.join(HERE, name), "w") as f:
+            json.dump({"source": src.format(variant), "connection_number": conn, "containers": records}, f, indent=0)
+        print(f"{name}: {len(cont)} containers, {sum(len(r['delivered']) for r in records)} deliveries, "
+              f"{divergent} reading past the datagram")
     with open(os.path.join(HERE, "dispatch_ref.bin"), "wb") as f:
         f.write(blob)
-    with open(os.path.join(HERE, "dispatch_ref.json"), "w") as f:
-        json.dump({"source": "oracle/_ref/net/plain/refnet_driver merged (the reference's net_peer::process_packet, "
-                             "net_peer.cpp:164-187), tests/golden/make_dispatch_ref.py",
-                   "connection_number": conn, "containers": records}, f, indent=0)
-    print(f"{len(cont)} containers, {sum(len(r['delivered']) for r in records)} deliveries, "
-          f"{divergent} reading past the datagram")
 
 
 def _reads_past(c, conn):

@@ -138,36 +138,92 @@ def load_ref_packet():
 MERGED_PROPERTY = 12  # PACKET_PROPERTY::MERGED (net_enums.h:60)
 
 
-def dispatch(wire_list, status):
+DISPATCH_TAIL_DATAGRAM, DISPATCH_TAIL_ZERO, DISPATCH_TAIL_LAYER = 0, 1, 2  # include/lnl_crc32c.h
+
+
+def ref_capacity(nbytes: int) -> int:
+    """buffer_size() of the reference's packet holding nbytes: net_packet()
+    allocates 2048 zero-filled bytes (ensure(1432), net_packet.h:46-49,
+    194-208) and resize() doubles it while it is short."""
+    cap = 2048
+    while cap < nbytes:
+        cap *= 2
+    return cap
+
+
+def dispatch_ex(wire_list, status, tail=DISPATCH_TAIL_DATAGRAM):
     """Packets a filtered burst delivers: (datagram index, offset within the
-    datagram, length) per packet.  Accepted datagrams are one packet (CRC
-    stripped); a MERGED container is cut as net_peer::process_packet does
-    (/root/reference/src/lnl/net_peer.cpp:164-187), bounded by the datagram
-    (the reference bounds by its pool buffer and reads stale bytes past it)."""
+    datagram, length, avail) per packet.  Accepted datagrams are one packet
+    (CRC stripped); a MERGED container is cut as net_peer::process_packet does
+    (/root/reference/src/lnl/net_peer.cpp:164-187).
+
+    tail DISPATCH_TAIL_DATAGRAM: the walk stops at the datagram's end.  The
+    other two walk the reference's own received buffer: bounded by its
+    capacity (:171, buffer_size() = 2048), with the bytes after the datagram
+    read as zeros (DISPATCH_TAIL_ZERO) or as the stripped CRC field and then
+    zeros (DISPATCH_TAIL_LAYER: INTEGRATION.md's receive_logic edit shrinks
+    the packet, the field stays in the buffer).  avail = the packet's bytes
+    that lie in the wire datagram; the rest are those zeros."""
     out = []
     for i, (w, st) in enumerate(zip(wire_list, status)):
         if st != INBOUND_ACCEPT:
             continue
         size = len(w) - 4
         if w[0] & 0x1F != MERGED_PROPERTY:
-            out.append((i, 0, size))
+            out.append((i, 0, size, size))
             continue
+        if tail == DISPATCH_TAIL_DATAGRAM:
+            pos = 1
+            while pos < size:
+                if pos + 2 > size:
+                    break
+                L = int(w[pos]) | (int(w[pos + 1]) << 8)
+                pos += 2
+                if L > size - pos or L == 0 or not packet_verify(int(w[pos]), L):
+                    break
+                out.append((i, pos, L, L))
+                pos += L
+            continue
+        lim = size + (4 if tail == DISPATCH_TAIL_LAYER else 0)
+        cap = ref_capacity(len(w))
+        buf = bytes(w[:lim]) + bytes(cap - lim)
         pos = 1
         while pos < size:
-            if pos + 2 > size:
-                break
-            L = int(w[pos]) | (int(w[pos + 1]) << 8)
+            L = buf[pos] | (buf[pos + 1] << 8)
             pos += 2
-            if L > size - pos or L == 0 or not packet_verify(int(w[pos]), L):
+            if cap - pos < L:
                 break
-            out.append((i, pos, L))
+            if L == 0 or not packet_verify(buf[pos], L):
+                break
+            out.append((i, pos, L, max(0, min(L, lim - pos))))
             pos += L
     return out
 
 
-def cut_merged(pkt):
-    """The entries of one MERGED packet under dispatch()'s rules (bounded by the
-    packet itself): [(offset, length)]."""
+def dispatch(wire_list, status):
+    """dispatch_ex under the datagram rule, as (datagram, offset, length)."""
+    return [(i, o, L) for i, o, L, _ in dispatch_ex(wire_list, status)]
+
+
+def cut_merged(pkt, ref_tail=False):
+    """The entries of one MERGED packet: [(offset, length)].  Bounded by the
+    packet itself (dispatch()'s datagram rule), or with ref_tail as the
+    reference cuts a packet it got from its pool (a fresh zero-filled buffer
+    of ref_capacity bytes, net_peer.cpp:175-176; offsets past the packet then
+    read zeros)."""
+    if ref_tail:
+        size = len(pkt)
+        cap = ref_capacity(size)
+        buf = bytes(pkt) + bytes(cap - size)
+        out, pos = [], 1
+        while pos < size:
+            L = buf[pos] | (buf[pos + 1] << 8)
+            pos += 2
+            if cap - pos < L or L == 0 or not packet_verify(buf[pos], L):
+                break
+            out.append((pos, L))
+            pos += L
+        return out
     out, pos, size = [], 1, len(pkt)
     while pos + 2 <= size:
         L = int(pkt[pos]) | (int(pkt[pos + 1]) << 8)
@@ -179,13 +235,13 @@ def cut_merged(pkt):
     return out
 
 
-def deliver(pkt, conn):
+def deliver(pkt, conn, ref_tail=False):
     """What net_peer::process_packet hands the user for one dispatched packet
     (/root/reference/src/lnl/net_peer.cpp:138-243), for the properties the
     dispatch fixture uses: dropped unless its connection number is conn (:156);
     UNRELIABLE -> [payload after the 1-byte header] (:240-243); MERGED -> its
-    entries (cut_merged: the product's datagram-bounded rule), each delivered
-    the same way; anything else -> nothing."""
+    entries (cut_merged: the datagram-bounded rule, or the reference's own
+    with ref_tail), each delivered the same way; anything else -> nothing."""
     pkt = bytes(pkt)
     if not pkt or ((pkt[0] & 0x60) >> 5) != conn:
         return []
@@ -194,9 +250,10 @@ def deliver(pkt, conn):
         return [pkt[1:]]
     if prop != MERGED_PROPERTY:
         return []
+    buf = pkt + bytes(ref_capacity(len(pkt)) - len(pkt)) if ref_tail else pkt
     out = []
-    for o, L in cut_merged(pkt):
-        out += deliver(pkt[o:o + L], conn)
+    for o, L in cut_merged(pkt, ref_tail):
+        out += deliver(buf[o:o + L], conn, ref_tail)
     return out
 
 

@@ -40,7 +40,7 @@ def test_header_declares_the_boundary():
               "lnl_dispatch_csr_dev", "lnl_inbound_filter_dispatch_csr_dev", "lnl_xor_layer", "lnl_xor_layer_csr_dev", "lnl_xor_layer_fixed_dev",
               "lnl_crc32c_append_host", "lnl_egress_send_batch", "lnl_crc32c_batch_host_ex",
               "lnl_inbound_filter_host_ex", "lnl_crc32c_append_host_ex", "lnl_stream_release",
-              "lnl_diag_fill_span_arrivals"):
+              "lnl_diag_fill_span_arrivals", "lnl_dispatch_csr_dev_ex", "lnl_inbound_filter_dispatch_csr_dev_ex"):
         assert s in syms
 
 
@@ -50,7 +50,7 @@ def test_library_exports_every_declared_symbol(pkg):
     exported = set(re.findall(r"\bT (lnl_\w+)", out))
     missing = [s for s in declared_symbols() if s not in exported]
     assert not missing, missing
-    assert pkg.lib().lnl_crc32c_abi_version() == 9
+    assert pkg.lib().lnl_crc32c_abi_version() == 10
 
 
 def test_ctypes_bindings_match_the_header(pkg):
@@ -209,3 +209,20 @@ def test_host_opts_checked_without_gpu(pkg):
     assert list(out) == [0, 0]
     with pytest.raises(ValueError):
         pkg.batch_host(np.zeros(64, np.uint8), np.array([0, 64], np.uint64), 0, streams=9)
+
+
+def test_dispatch_opts_rejected_before_device_work(pkg):
+    """lnl_dispatch_csr_dev_ex / lnl_inbound_filter_dispatch_csr_dev_ex check
+    their lnl_dispatch_opts first: -EINVAL for a short struct, an unknown tail
+    rule or a nonzero reserved word, without touching a device (no GPU here)."""
+    import ctypes
+    from litenetlibpp_amd._lib import DispatchOpts
+    L = pkg.lib()
+    total = ctypes.c_uint32(0)
+    bad = [DispatchOpts(4, 1), DispatchOpts(ctypes.sizeof(DispatchOpts), 3),
+           DispatchOpts(ctypes.sizeof(DispatchOpts), 1, (ctypes.c_uint32 * 2)(0, 1))]
+    for o in bad:
+        for f in (L.lnl_dispatch_csr_dev_ex, L.lnl_inbound_filter_dispatch_csr_dev_ex):
+            rc = f(None, None, 0, None, None, None, None, None, 0, ctypes.addressof(total), ctypes.byref(o), None)
+            assert rc == -22, (f.__name__, rc)
+    assert pkg.DISPATCH_TAIL_DATAGRAM == 0 and pkg.DISPATCH_TAIL_ZERO == 1 and pkg.DISPATCH_TAIL_LAYER == 2

@@ -600,18 +600,27 @@ def test_append_host_egress_loopback(P):
 
 
 @pytest.mark.parametrize("replicas,fused", [(1, False), (1, True), (150, False), (150, True)])
-def test_dispatch_reference_fixture(P, replicas, fused):
+@pytest.mark.parametrize("tail", ["datagram", "zero", "layer"])
+def test_dispatch_reference_fixture(P, replicas, fused, tail):
     """The MERGED cut against the REFERENCE's own process_packet
-    (tests/golden/dispatch_ref.*, made by running the reference's net_manager:
-    tests/golden/make_dispatch_ref.py): every container of the fixture, as a
-    wire datagram with its CRC, through lnl_inbound_filter_csr_dev +
-    lnl_dispatch_csr_dev or the fused lnl_inbound_filter_dispatch_csr_dev;
-    the packets each container gives, handed to the caller's process_packet
-    (oracle.deliver), must be exactly what the reference delivered -- or, where
-    the reference reads past the datagram, exactly the deliveries before that
-    read.  150 replicas (17,250 datagrams, shuffled) take the span path."""
-    from test_dispatch_ref import expected, load_fixture, with_crc
-    cont, conn, recs = load_fixture()
+    (tests/golden/dispatch_ref*.json, made by running the reference's
+    net_manager: tests/golden/make_dispatch_ref.py): every container of the
+    fixture, as a wire datagram with its CRC, through lnl_inbound_filter_csr_dev
+    + lnl_dispatch_csr_dev_ex or the fused lnl_inbound_filter_dispatch_csr_dev_ex;
+    the packets each container gives (their in-burst bytes, then the zero fill
+    of d_pkt_avail), handed to the caller's process_packet (oracle.deliver),
+    must be exactly what the reference delivered:
+      zero   every delivery of the plain reference (dispatch_ref.json), the
+             zero-padded packets included (LNL_DISPATCH_TAIL_ZERO)
+      layer  every delivery of the reference with INTEGRATION.md's layer
+             compiled in (dispatch_ref_layer.json: the CRC field, then zeros;
+             LNL_DISPATCH_TAIL_LAYER)
+      datagram  the default rule: the deliveries before the first read past
+             the datagram, and all of them for every other container.
+    150 replicas (17,250 datagrams, shuffled) take the span path."""
+    from test_dispatch_ref import expected, load_fixture, packet_bytes, reference_deliveries, with_crc
+    mode = {"datagram": P.DISPATCH_TAIL_DATAGRAM, "zero": P.DISPATCH_TAIL_ZERO, "layer": P.DISPATCH_TAIL_LAYER}[tail]
+    cont, conn, recs = load_fixture("layer" if tail == "layer" else "plain")
     rng = np.random.default_rng(60 + replicas)
     order = np.concatenate([rng.permutation(len(cont)) for _ in range(replicas)])
     wires = [with_crc(cont[k]) for k in order]
@@ -620,16 +629,21 @@ def test_dispatch_reference_fixture(P, replicas, fused):
     data = np.frombuffer(bytes(lead) + b"".join(wires) + bytes(5), dtype=np.uint8)
     d, o = dev(data), dev(off.view(np.int64), torch.int64)
     if fused:
-        status, start, length, parent = P.filter_dispatch(d, o)
+        status, start, length, parent, avail = P.filter_dispatch(d, o, tail=mode, avail=True)
     else:
         status = P.inbound_filter(d, o)
-        start, length, parent = P.dispatch(d, o, status)
+        start, length, parent, avail = P.dispatch(d, o, status, tail=mode, avail=True)
     assert bool((status == P.INBOUND_ACCEPT).all())
     got = [[] for _ in wires]
-    for s0, L, i in zip(start.cpu().numpy(), length.cpu().numpy(), parent.cpu().numpy()):
-        got[int(i)] += oracle.deliver(data[int(s0):int(s0) + int(L)], conn)
-    bad = [j for j, k in enumerate(order) if got[j] != expected(recs[k])]
+    padded = 0
+    for s0, L, i, av in zip(start.cpu().numpy(), length.cpu().numpy(), parent.cpu().numpy(), avail.cpu().numpy()):
+        assert 0 <= av <= L
+        padded += int(av < L)
+        got[int(i)] += oracle.deliver(packet_bytes(data, int(s0), int(L), int(av)), conn, ref_tail=mode != 0)
+    want = [reference_deliveries(recs[k]) if mode else expected(recs[k]) for k in order]
+    bad = [j for j in range(len(wires)) if got[j] != want[j]]
     assert not bad, [(j, int(order[j])) for j in bad[:8]]
+    assert (padded > 0) == (mode != 0)
 
 
 def _merged(rng, parts, mode):
@@ -689,6 +703,78 @@ def test_dispatch_merged_containers(P, n):
     # a capped call writes the first `cap` packets and still reports the total
     s2, l2, p2 = P.dispatch(d, o, status, cap=7)
     assert p2.cpu().numpy().tolist() == [e[0] for e in exp[:7]]
+
+
+def _tail_wires(P, rng, n):
+    """Containers whose walk runs past the datagram in every way the tail
+    rules see: truncated entries, a size field in the last byte, a last
+    entry longer than what is left, entries reaching past the 2048-byte
+    capacity, more than 8 entries before the cut, nested containers, plain
+    datagrams and corrupted CRCs."""
+    layer = P.Crc32cLayer()
+    sub = lambda m: bytes([int(rng.choice([0x00, 0x01, 0x03]))]) + \
+        rng.integers(0, 256, max(m - 1, 0), dtype=np.uint8).tobytes()
+    wires = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.7:
+            parts = [sub(int(rng.integers(1, 90))) for _ in range(int(rng.integers(0, 12)))]
+            body = bytearray(_merged(rng, parts, "ok"))
+            kind = rng.integers(0, 6)
+            if kind == 0 and len(body) > 2:
+                body = body[:int(rng.integers(2, len(body)))]            # truncated anywhere
+            elif kind == 1:
+                body += bytes([int(rng.integers(0, 256))])              # size field in the last byte
+            elif kind == 2:
+                body += int(rng.integers(1, 3000)).to_bytes(2, "little") + sub(int(rng.integers(0, 5)))
+            elif kind == 3:
+                body += int(rng.integers(1, 8)).to_bytes(2, "little")   # a size field, nothing after it
+            body = bytes(body)
+            if rng.random() < 0.05:
+                body = _merged(rng, [body], "ok")
+        else:
+            body = sub(int(rng.integers(0, 300)))
+        w = bytearray(layer.process_outbound(body))
+        if rng.random() < 0.02:
+            w[int(rng.integers(0, len(w)))] ^= 0x10
+        wires.append(bytes(w))
+    return wires
+
+
+@pytest.mark.parametrize("tail", ["zero", "layer"])
+@pytest.mark.parametrize("n", [500, 30000])
+def test_dispatch_tail_rules(P, n, tail):
+    """lnl_dispatch_csr_dev_ex and lnl_inbound_filter_dispatch_csr_dev_ex under
+    the reference's tail rules (the walk bounded by the zero-filled 2048-byte
+    buffer, net_peer.cpp:167-183): every packet's start, length and in-burst
+    bytes equal oracle.dispatch_ex's, and the datagram rule still gives
+    oracle.dispatch's packets on the same burst."""
+    mode = P.DISPATCH_TAIL_ZERO if tail == "zero" else P.DISPATCH_TAIL_LAYER
+    rng = np.random.default_rng(3100 + n + mode)
+    wires = _tail_wires(P, rng, n)
+    off = np.concatenate([[0], np.cumsum([len(w) for w in wires])]).astype(np.uint64)
+    # the bytes after the batch read as a container: a tail walk must never take them
+    trail = bytes([0x0C]) + b"".join(bytes([1, 0, 0]) for _ in range(40))
+    blob = np.frombuffer(b"".join(wires) + trail, np.uint8)
+    d, o = dev(blob), dev(off.view(np.int64), torch.int64)
+    status = P.inbound_filter(d, o)
+    st = status.cpu().numpy()
+    exp = oracle.dispatch_ex([np.frombuffer(w, np.uint8) for w in wires], st, mode)
+    assert sum(1 for e in exp if e[3] < e[2]) > n // 100          # zero-padded packets occur
+    for fused in (False, True):
+        if fused:
+            st2, start, length, parent, avail = P.filter_dispatch(d, o, tail=mode, avail=True)
+            assert torch.equal(st2, status)
+        else:
+            start, length, parent, avail = P.dispatch(d, o, status, tail=mode, avail=True)
+        got = [e + (int(a),) for e, a in zip(_packets(off, start, length, parent), avail.cpu().numpy())]
+        assert got == exp, next(((k, g, e) for k, (g, e) in enumerate(zip(got, exp)) if g != e), None)
+    # the default rule on the same burst: the datagram-bounded cut, avail == len
+    s3, l3, p3, a3 = P.filter_dispatch(d, o, avail=True)[1:]
+    assert _packets(off, s3, l3, p3) == oracle.dispatch([np.frombuffer(w, np.uint8) for w in wires], st)
+    assert torch.equal(a3, l3)
+    with pytest.raises(ValueError):
+        P.dispatch(d, o, status, tail=7)
 
 
 def test_dispatch_records_and_rewalk(P):
