@@ -25,8 +25,10 @@ CRC words written; CSR adds 8 N offset bytes; the xor workload reads and writes
 2 sum(L)) over the average launch duration measured with one HIP event pair
 around the K launches on the launch stream; peak 8.0 TB/s (MI355X HBM3E
 nameplate).  traffic: HBM bytes per launch from the builder's rocprofv3 PMC
-passes (profiles/traffic_<workload>.json; FETCH_SIZE x2 gfx950 correction +
-WRITE_SIZE), labelled as such -- it is not measured inside this run.
+passes (profiles/traffic_<workload>.json; FETCH_SIZE x its access shape's
+factor -- x2 for wide streaming reads, x1 for the dispatch walk's random
+sectors, calibrated in profiles/fetch_calibration.json -- + WRITE_SIZE),
+labelled as such -- it is not measured inside this run.
 cpu_baseline: the oracle's batch CRC (SSE4.2 crc32 instruction, OpenMP) timed
 on this host over the WHOLE batch (copied to host memory, untimed), on one
 core and on every core this process may run on (rank 0, N = 1); the checker
@@ -650,6 +652,8 @@ def main():
             line["roofline"]["sector_granular_bytes_per_launch"] = w["line_bytes"]
             line["roofline"]["sector_granular_achieved"] = round(lb, 1)
             line["roofline"]["sector_granular_frac"] = round(lb / HBM_PEAK_GBS, 4)
+            if traffic:  # (the walk's FETCH_SIZE factor is calibrated: profiles/fetch_calibration.json)
+                line["roofline"]["traffic_over_sector_floor"] = round(traffic / w["line_bytes"], 3)
         if not DRY:
             probe = hbm_probe_peak(w["data"], device)
             if probe:

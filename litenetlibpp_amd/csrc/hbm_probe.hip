@@ -249,6 +249,54 @@ __global__ __launch_bounds__(256) void run_read(const uint8_t* __restrict__ p, u
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// FETCH_SIZE calibration for dword-granular random reads (the dispatch walk's
+// access shape, lnl_dispatch.hip): thread t reads
+// `words` adjacent dwords (1 or 2: load3's aligned pair) at dword offset
+// (t & 7) * 2 of 64-byte sector perm(t) = (t * P) mod S, P odd and S a power
+// of two, so that `n` threads touch n distinct sectors exactly once: the
+// bytes that must cross the memory bus are n x 64 (one sector each) and the
+// kernel wants 4 words x n of them.
+__global__ __launch_bounds__(256) void sector_read(const uint32_t* __restrict__ p, uint64_t sectors_mask,
+                                                   uint32_t n, uint32_t words, uint32_t* sink) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= n) return;
+    const uint64_t sec = ((uint64_t)t * 0x9E3779B97F4A7C15ull) & sectors_mask;  // odd multiplier: a permutation
+    const uint32_t* q = p + sec * 16u + (t & 7u) * 2u;
+    uint32_t v = q[0];
+    if (words > 1u) v ^= q[1];
+    if (v == 0x9E3779B9u) sink[0] = v;
+}
+
+// the same bytes read as one dword per lane, consecutive lanes on consecutive
+// dwords (256 B per wave-instruction: the dispatch emit pass's record reads)
+__global__ __launch_bounds__(256) void dword_stream(const uint32_t* __restrict__ p, uint64_t n4, uint32_t* sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256u) acc ^= p[i];
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+extern "C" int lnl_probe_dword_stream(const void* d, size_t bytes, uint32_t* d_sink, void* stream) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipLaunchKernelGGL(dword_stream, dim3(cus * 8), dim3(256), 0, (hipStream_t)stream, (const uint32_t*)d,
+                       (uint64_t)(bytes / 4), d_sink);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// n distinct random 64-byte sectors of the first `bytes` (a power of two of
+// sectors is used: the largest that fits), `words` dwords each; returns the
+// sector count used, or a negative code.
+extern "C" int64_t lnl_probe_sector_read(const void* d, size_t bytes, uint32_t n, uint32_t words, uint32_t* d_sink,
+                                         void* stream) {
+    uint64_t sectors = 1;
+    while (sectors * 2u * 64u <= bytes) sectors *= 2u;
+    if (n == 0 || n > sectors || words < 1 || words > 2) return -22;
+    hipLaunchKernelGGL(sector_read, dim3((n + 255u) / 256u), dim3(256), 0, (hipStream_t)stream,
+                       (const uint32_t*)d, sectors - 1u, n, words, d_sink);
+    return hipGetLastError() == hipSuccess ? (int64_t)sectors : -5;
+}
+
 extern "C" int lnl_probe_stream_read(const void* d, size_t bytes, uint32_t* d_sink, void* stream, int form) {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);

@@ -27,6 +27,24 @@ PRODUCT_KERNELS = ("crc32c_", "bucket_count", "bucket_scatter", "bucket_hist", "
                    "xor_chunk_map", "span_prep", "append_")
 
 
+# FETCH_SIZE's bytes per byte read, by access shape (MI355X_MICROARCH.md HBM
+# section: gfx950 counts half of a wide coalesced streaming read; the other
+# shapes calibrated by tools/fetch_calibration.py on known byte counts,
+# profiles/fetch_calibration.json).  Kernels not listed read in wide streams.
+FETCH_SHAPE = {
+    "dispatch_count_kernel": "random_dword_sector",   # the MERGED walk: dword pairs at random 64-B sectors
+    "dispatch_emit_kernel": "dword_stream",           # records and counts, one dword per lane
+}
+
+
+def fetch_factor(kernel):
+    cal = os.path.join(ROOT, "profiles", "fetch_calibration.json")
+    shape = next((v for k, v in FETCH_SHAPE.items() if k in kernel), "wide_stream_16B")
+    if shape == "wide_stream_16B" or not os.path.exists(cal):
+        return 2.0, shape
+    return float(json.load(open(cal))["bytes_per_fetch_byte"][shape]), shape
+
+
 def main():
     tag, wl = sys.argv[1], sys.argv[2]
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{wl}")
@@ -42,6 +60,8 @@ def main():
     # kernel plus, for CSR, its bucket pre-pass), counter totals divided by the
     # dispatch count of the dominant product kernel (the one with the most time)
     pmc_tot = {}
+    fetch_bytes = 0.0   # FETCH_SIZE x its shape's factor, per kernel
+    shapes = {}
     kernels = set()
     trace_stats = None
     for part in ("trace", "fetch", "write", "clk", "sq"):
@@ -71,15 +91,22 @@ def main():
                 kernels.add(short(name))
                 for cn, vals in cs.items():
                     pmc_tot[cn] = pmc_tot.get(cn, 0.0) + sum(vals) / pass_calls
+                    if cn == "FETCH_SIZE":
+                        f, shape = fetch_factor(name)
+                        shapes[short(name)] = [shape, f]
+                        fetch_bytes += sum(vals) / pass_calls * 1024 * f
     pmc_means = dict(pmc_tot)
     with open(os.path.join(dst, f"{tag}_{wl}_summary.md"), "w") as f:
         f.write("\n".join(md))
-    fetch = pmc_means["FETCH_SIZE"] * 1024 * 2
+    fetch = fetch_bytes
     write = pmc_means["WRITE_SIZE"] * 1024
     tr = {"kernel": crc_kernel, "kernels_per_call": sorted(kernels), "workload": wl, "hbm_bytes_per_launch": round(fetch + write),
-          "fetch_bytes": round(fetch), "fetch_size_raw_bytes": round(fetch / 2), "write_bytes": round(write),
-          "how": "rocprofv3 PMC passes (tools/profile_round.sh): FETCH_SIZE (KiB) x 1024 x 2 "
-                 "(gfx950 counts half of wide streaming reads) + WRITE_SIZE (KiB) x 1024, summed over the product kernels of one API call",
+          "fetch_bytes": round(fetch), "fetch_size_raw_bytes": round(pmc_means["FETCH_SIZE"] * 1024),
+          "write_bytes": round(write), "fetch_shapes": shapes,
+          "how": "rocprofv3 PMC passes (tools/profile_round.sh): per product kernel FETCH_SIZE (KiB) x 1024 x its "
+                 "access shape's factor (x 2 for wide streaming reads, MI355X_MICROARCH.md; the others from "
+                 "profiles/fetch_calibration.json, tools/fetch_calibration.py) + WRITE_SIZE (KiB) x 1024, summed over "
+                 "the product kernels of one API call",
           "source": f"profiles/{tag}_{wl}_summary.md"}
     with open(os.path.join(dst, f"traffic_{wl}.json"), "w") as f:
         json.dump(tr, f, indent=1)
