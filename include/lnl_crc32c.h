@@ -342,8 +342,10 @@ int lnl_stream_release(void* hip_stream);
 /* Diagnostics (tests): fills every wave-batch exchange arrival word of the span
  * scratch kept for `hip_stream` with `value`, as an aborted call could leave
  * it.  Synchronises the stream first; blocking.  -ENOENT when no CSR call has
- * run on the stream yet.  Later calls must be unaffected (the arrival words
- * pair by per-call epoch, crc32c_span.h). */
+ * run on the stream yet; -EINVAL (nothing written) for a value no earlier call
+ * could have left: an epoch (value >> 2) past the calls made on the stream.
+ * Later calls must be unaffected (the arrival words pair by per-call epoch,
+ * crc32c_span.h). */
 int lnl_diag_fill_span_arrivals(void* hip_stream, uint64_t value);
 
 /* Message for the last failure on the calling thread ("" if none). */

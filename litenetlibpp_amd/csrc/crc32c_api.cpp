@@ -238,9 +238,16 @@ int csr_path() {
 // stream in this library's launches (it is not built with per-thread default
 // streams), one stream for all threads.
 // Bound.  At most LNL_STREAM_CACHE streams' scratch is kept per device and map;
-// beyond that the least recently used entry is freed (after a device-wide
-// synchronize, since its stream may have been destroyed).  lnl_stream_release
-// frees a stream's entries explicitly, stream-ordered.
+// beyond that the least recently used entry is freed.  Its stream may have
+// been destroyed, so the free goes on a library-owned stream of the device,
+// behind the entry's last use: every call records an event on its stream once
+// it has enqueued everything that reads the entry, and the eviction makes the
+// library stream wait for that event (no host or device-wide synchronise, and
+// a caller in stream capture is not disturbed by another stream's eviction).
+// lnl_stream_release frees a stream's entries explicitly, stream-ordered.
+// A call holds the cache's mutex from its choice of the entry until that event
+// is recorded, so an entry is never evicted or released between a call's
+// launches (with_span_scratch, with_xor_map).
 struct StreamKey {
     int dev;
     hipStream_t st;
@@ -262,9 +269,23 @@ StreamKey stream_key(hipStream_t st) {
 struct SpanScratch {
     uint32_t* buf = nullptr;
     size_t words = 0;
-    uint64_t calls = 0;  // span path: calls made on it (the control block parity and the exchange epoch)
-    uint64_t used = 0;   // LRU tick
+    uint64_t calls = 0;          // span path: calls made on it (the control block parity and the exchange epoch)
+    uint64_t used = 0;           // LRU tick
+    hipEvent_t done = nullptr;   // recorded after the last call's launches that read buf
 };
+
+// the library's own stream on the current device (evictions free on it)
+hipStream_t library_stream(int dev) {
+    static std::mutex mu;
+    static hipStream_t st[kMaxDevices] = {};
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+    if (!st[dev] && hipStreamCreateWithFlags(&st[dev], hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        st[dev] = nullptr;
+    }
+    return st[dev];
+}
 
 struct ScratchCache {
     std::mutex mu;
@@ -273,11 +294,18 @@ struct ScratchCache {
 
     // the entry for st, at least `words` long (the first zero_words zeroed
     // whenever it is (re)allocated, and its call count restarted); evicts
-    // beyond the bound
+    // beyond the bound.  Caller holds mu.
     int get(hipStream_t st, size_t words, size_t zero_words, SpanScratch** out) {
         const StreamKey key = stream_key(st);
         SpanScratch& s = m[key];
         s.used = ++tick;
+        if (!s.done) {
+            hipError_t e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+            if (e != hipSuccess) {
+                s.done = nullptr;
+                return hip_fail(e, "hipEventCreate");
+            }
+        }
         if (s.words < words) {
             const size_t grow = words + words / 4;  // headroom: batches of similar sizes reuse it
             if (s.buf) (void)hipFreeAsync(s.buf, st);
@@ -295,6 +323,11 @@ struct ScratchCache {
         return 0;
     }
 
+    // a call's launches that read the entry are enqueued on st.  Caller holds mu.
+    static void used_by(SpanScratch* s, hipStream_t st) {
+        if (s && s->done) (void)hipEventRecord(s->done, st);
+    }
+
     void evict(const StreamKey& keep) {
         size_t on_dev = 0;
         for (auto& kv : m) on_dev += kv.first.dev == keep.dev;
@@ -306,9 +339,19 @@ struct ScratchCache {
                 victim = it;
         }
         if (victim == m.end()) return;
-        // its stream may be gone: drain the device, then free on the null stream
-        (void)hipDeviceSynchronize();
-        if (victim->second.buf) (void)hipFreeAsync(victim->second.buf, nullptr);
+        // its stream may be gone: free on the library stream, behind its last use
+        hipStream_t ls = library_stream(keep.dev);
+        SpanScratch& v = victim->second;
+        if (ls && v.done) (void)hipStreamWaitEvent(ls, v.done, 0);
+        if (v.buf) {
+            if (ls)
+                (void)hipFreeAsync(v.buf, ls);
+            else {
+                if (v.done) (void)hipEventSynchronize(v.done);
+                (void)hipFree(v.buf);
+            }
+        }
+        if (v.done) (void)hipEventDestroy(v.done);
         m.erase(victim);
     }
 
@@ -317,6 +360,7 @@ struct ScratchCache {
         auto it = m.find(stream_key(st));
         if (it == m.end()) return;
         if (it->second.buf) (void)hipFreeAsync(it->second.buf, st);
+        if (it->second.done) (void)hipEventDestroy(it->second.done);
         m.erase(it);
     }
 };
@@ -329,15 +373,18 @@ int span_scratch(hipStream_t st, size_t words, size_t zero_words, SpanScratch** 
 
 // The CSR XOR kernel's chunk map (lnl_xor.hip), kept per (device, stream) like
 // the span scratch: each call's map kernel rewrites the words its XOR kernel
-// reads, in stream order, so calls on one stream share it.
+// reads, in stream order, so calls on one stream share it.  fn(map) enqueues
+// the launches that use it, under the cache's mutex.
 ScratchCache g_xor_cache;
 
-int xor_map_scratch(hipStream_t st, size_t words, uint32_t** buf) {
+template <typename F>
+int with_xor_map(hipStream_t st, size_t words, F&& fn) {
     std::lock_guard<std::mutex> lk(g_xor_cache.mu);
     SpanScratch* s = nullptr;
     if (int rc = g_xor_cache.get(st, words, 0, &s)) return rc;
-    *buf = s->buf;
-    return 0;
+    const int rc = fn(s->buf);
+    ScratchCache::used_by(s, st);
+    return rc;
 }
 
 // CSR batches (product path): the span kernel (crc32c_span.hip: every line read
@@ -347,8 +394,13 @@ int xor_map_scratch(hipStream_t st, size_t words, uint32_t** buf) {
 // when the span kernel does not take it.
 // (span_mode: kSpanCrc -> out[i]; kSpanVerify / kSpanFilter -> ok[i], the
 // overflow datagrams through the batch kernel in verify mode)
+int no_after(const uint32_t*) { return 0; }
+
+// (after(ctl): launches that read this call's span control block, enqueued
+// before the cache's mutex is released -- the fused dispatch's fix-up)
+template <typename F = decltype(&no_after)>
 int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t st, uint32_t span_mode = lnl::kSpanCrc,
-                    uint32_t* walk_blocks = nullptr, const uint32_t** span_ctl = nullptr) {
+                    uint32_t* walk_blocks = nullptr, F&& after = &no_after) {
     lnl::SpanArgs g{};
     g.mode = span_mode;
     g.wblk = walk_blocks;  // filter + dispatch: the MERGED walk in the same pass
@@ -370,18 +422,20 @@ int launch_csr_span(const DeviceState& S, const lnl::BatchArgs& a, hipStream_t s
     // batch-kernel launch below leaves nothing stale for the next call.
     lnl::span_scratch_layout(g, sc->buf, (uint32_t)(sc->calls & 1u));
     g.epoch = sc->calls + 1u;
-    if (span_ctl) *span_ctl = g.ctl;
     hipError_t e = lnl::launch_span(g, S.cus, st);
     if (e != hipSuccess) return hip_fail(e, "span kernel launch");
     ++sc->calls;
-#if defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 32)
-    return 0;  // diagnostic build only: no batch kernel (overflow datagrams left unwritten)
-#endif
+    int rc = 0;
+#if !(defined(LNL_SPAN_DIAG) && (LNL_SPAN_DIAG & 32))  // (diagnostic build only: no batch kernel)
     lnl::BatchArgs o = a;
     o.perm = g.ovf;
     o.perm_n = g.ctl + 1;
     o.span_ctl = g.ctl;
-    return launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st, LNL_SPAN_FIX_WGS);
+    rc = launch(S, o, span_mode == lnl::kSpanCrc ? lnl::kModeCsr : lnl::kModeVerify, st, LNL_SPAN_FIX_WGS);
+#endif
+    if (rc == 0) rc = after(g.ctl);
+    ScratchCache::used_by(sc, st);
+    return rc;
 }
 
 int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st) {
@@ -461,6 +515,11 @@ extern "C" int lnl_diag_fill_span_arrivals(void* hip_stream, uint64_t value) {
     std::lock_guard<std::mutex> lk(g_span_cache.mu);
     auto it = g_span_cache.m.find(stream_key(st));
     if (it == g_span_cache.m.end() || !it->second.buf) return fail(-ENOENT, "no span scratch kept for this stream");
+    // only what an earlier call could have left: an epoch up to the calls
+    // made (a later one could pair with a future call's arrival)
+    if ((value >> 2) > it->second.calls)
+        return fail(-EINVAL, "arrival epoch %llu is past the %llu calls made on this stream",
+                    (unsigned long long)(value >> 2), (unsigned long long)it->second.calls);
     const uint32_t waves = (uint32_t)S->cus * (uint32_t)(lnl::kSpanThreads / 64) * LNL_SPAN_ROUNDS;
     const size_t blocks = lnl::span_max_segments(waves) / 64u;
     hipError_t e = hipStreamSynchronize(st);
@@ -652,7 +711,7 @@ int host_plan(const lnl_host_opts* o, HostPlan* p) {
 // Slot k holds at least these sizes (its stream created on first use; buffers
 // regrown only when a call needs more).  Freeing a slot's buffers is safe
 // here: the previous call on this device drained every slot's stream.
-int slot_ready(HostSlot& s, size_t need_bytes, size_t need_n, size_t need_wire) {
+int slot_ready(HostSlot& s, size_t need_bytes, size_t need_n, size_t need_wire, bool stage) {
     hipError_t e;
     if (!s.stream && (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
         return hip_fail(e, "hipStreamCreate");
@@ -671,7 +730,7 @@ int slot_ready(HostSlot& s, size_t need_bytes, size_t need_n, size_t need_wire) 
         s.cap_bytes = nb;
         s.cap_n = need_n;
     }
-    if (need_n * 4 > s.cap_stage) {  // pinned result staging (used for pageable outputs)
+    if (stage && need_n * 4 > s.cap_stage) {  // pinned result staging: only for a pageable output array
         (void)hipHostFree(s.h_stage);
         s.h_stage = nullptr;
         s.cap_stage = 0;
@@ -696,13 +755,20 @@ int slot_ready(HostSlot& s, size_t need_bytes, size_t need_n, size_t need_wire) 
 // copy into it directly.  Into pageable memory a D2H goes through the runtime's
 // own staging and holds up the pipeline (config 5 with a pageable CRC array:
 // 50.2 against 53.9 GB/s, tools/host_path_probe.py).
-bool host_pinned(const void* p) {
-    hipPointerAttribute_t at{};
-    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-        (void)hipGetLastError();  // (pageable memory: an error, not sticky)
-        return false;
-    }
-    return at.type == hipMemoryTypeHost;
+// Both ends of the range are checked (a range that starts in a pinned block
+// and runs on into pageable memory stages); a range whose two ends are pinned
+// is taken as pinned throughout -- one hipHostMalloc / hipHostRegister block,
+// as the callers allocate it.
+bool host_pinned(const void* p, size_t bytes) {
+    auto one = [](const void* q) {
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, q) != hipSuccess) {
+            (void)hipGetLastError();  // (pageable memory: an error, not sticky)
+            return false;
+        }
+        return at.type == hipMemoryTypeHost;
+    };
+    return one(p) && (bytes <= 1 || one((const uint8_t*)p + bytes - 1));
 }
 
 // A slot's staged results of its previous chunk to the caller's array (the
@@ -765,8 +831,12 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         i = j;
     }
     const size_t need_wire = mode == kHostAppend ? need_bytes + (size_t)need_n * LNL_CRC32C_LAYER_EXTRA : 0;
+    // the small result arrays (CRCs, statuses, append's optional CRCs) go
+    // through the slots' pinned staging when the caller's are pageable
+    void* const small_out = mode == kHostAppend ? (void*)h_crc : h_out;
+    const bool stage = small_out && !host_pinned(small_out, (size_t)n * (filter ? 1u : 4u));
     for (int k = 0; k < ns; ++k)
-        if (int rc = slot_ready(S->slot[k], need_bytes, need_n, need_wire)) return rc;
+        if (int rc = slot_ready(S->slot[k], need_bytes, need_n, need_wire, stage)) return rc;
     // after the first enqueue, every error path drains the streams first: the
     // caller may free h_base / h_out as soon as we return
     auto drained = [&](int rc) {
@@ -776,10 +846,6 @@ int host_batch(const uint8_t* h_base, const uint64_t* h_off, uint32_t n, void* h
         }
         return rc;
     };
-    // the small result arrays (CRCs, statuses, append's optional CRCs) go
-    // through the slots' pinned staging when the caller's are pageable
-    void* const small_out = mode == kHostAppend ? (void*)h_crc : h_out;
-    const bool stage = small_out && !host_pinned(small_out);
     uint32_t i = 0;
     int k = 0;
     while (i < n) {
@@ -1056,11 +1122,11 @@ extern "C" int lnl_inbound_filter_dispatch_csr_dev_ex(const uint8_t* d_base, con
     b.n = n;
     b.ok = d_status;
     b.filter = 1u;
-    const uint32_t* span_ctl = nullptr;
-    int rc = launch_csr_span(*S, b, st, lnl::kSpanFilter, blk, &span_ctl);
-    a.span_ctl = span_ctl;  // [2] != 0: the span kernel walked the batch
-    if (rc == 0 && (e = lnl::launch_dispatch_walked(a, tmp, scan_bytes, st)) != hipSuccess)
-        rc = hip_fail(e, "dispatch launch");
+    int rc = launch_csr_span(*S, b, st, lnl::kSpanFilter, blk, [&](const uint32_t* span_ctl) {
+        a.span_ctl = span_ctl;  // [2] != 0: the span kernel walked the batch
+        hipError_t le = lnl::launch_dispatch_walked(a, tmp, scan_bytes, st);
+        return le == hipSuccess ? 0 : hip_fail(le, "dispatch launch");
+    });
     e = hipFreeAsync(scratch, st);
     if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
     return rc;
@@ -1135,10 +1201,10 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
 #define LNL_XOR_GRID_WGS 4  // workgroups per CU (112 VGPRs: 4 waves per SIMD)
 #endif
     if (LNL_XOR_CSR_FLAT == 3 && d_off) {
-        uint32_t* map = nullptr;
-        if (int rc = xor_map_scratch((hipStream_t)hip_stream, (size_t)n + 1u, &map)) return rc;
-        hipError_t e = lnl::launch_xor_csr_grid(a, map, n + 1u, S->cus * LNL_XOR_GRID_WGS, (hipStream_t)hip_stream);
-        return e == hipSuccess ? 0 : hip_fail(e, "xor csr grid launch");
+        return with_xor_map((hipStream_t)hip_stream, (size_t)n + 1u, [&](uint32_t* map) {
+            hipError_t e = lnl::launch_xor_csr_grid(a, map, n + 1u, S->cus * LNL_XOR_GRID_WGS, (hipStream_t)hip_stream);
+            return e == hipSuccess ? 0 : hip_fail(e, "xor csr grid launch");
+        });
     }
 #ifndef LNL_XOR_STREAM_WGS
 #define LNL_XOR_STREAM_WGS 6  // workgroups per CU

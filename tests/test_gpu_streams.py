@@ -139,24 +139,39 @@ def test_host_opts_rejected(P):
 
 def test_span_stale_arrival_words_never_pair(P):
     """The span kernel's wave-batch exchange pairs by the call's epoch: arrival
-    words filled with whatever an aborted call might leave (the old protocol
-    needed them at 0 between calls) change nothing in the next calls."""
+    words filled with whatever an aborted call might leave -- either side, any
+    epoch up to the calls made so far (the old protocol needed them at 0
+    between calls) -- change nothing in the next calls; a value with a later
+    epoch is refused (it could pair with a future call's own arrival)."""
     data, off = csr_batch(800, 200_000)
     d, o = dev(data), dev(off.view(np.int64), torch.int64)
     exp = oracle.batch_csr(data, off)
-    s = torch.cuda.current_stream()
-    assert np.array_equal(u32(P.batch_csr(d, o)), exp)
-    for value in (1, 2, 3, 5, 0xFFFFFFFFFFFFFFFF, (1 << 40) | 1, (7 << 2) | 1):
+    s = torch.cuda.Stream()  # (its own scratch: the epoch count starts here)
+    torch.cuda.synchronize()
+    assert np.array_equal(u32(P.batch_csr(d, o, stream=s)), exp)
+    calls = 1
+    for value in (1, 2, 3, 5, 6, 7, (2 << 2) | 1, (3 << 2) | 2, (7 << 2) | 1, (9 << 2) | 2):
         rc = P.lib().lnl_diag_fill_span_arrivals(s.cuda_stream, value)
-        assert rc == 0, P.lib().lnl_crc32c_last_error()
+        if (value >> 2) > calls:  # an epoch no earlier call reached: refused, nothing written
+            assert rc == -22, rc
+        else:
+            assert rc == 0, P.lib().lnl_crc32c_last_error()
+        calls += 2
         for _ in range(2):
             out = torch.full((off.size - 1,), -1, dtype=torch.int32, device="cuda")
-            assert np.array_equal(u32(P.batch_csr(d, o, out=out)), exp), hex(value)
+            torch.cuda.synchronize()
+            got = P.batch_csr(d, o, out=out, stream=s)
+            s.synchronize()
+            assert np.array_equal(u32(got), exp), hex(value)
     # and the status path (verify mode on the same scratch)
     wd, woff, wexp = wire_batch(P, 801, 30_000)
     assert P.lib().lnl_diag_fill_span_arrivals(s.cuda_stream, 1) == 0
-    got = P.inbound_filter(dev(wd), dev(woff.view(np.int64), torch.int64))
+    wd_d, woff_d = dev(wd), dev(woff.view(np.int64), torch.int64)
+    torch.cuda.synchronize()
+    got = P.inbound_filter(wd_d, woff_d, stream=s)
+    s.synchronize()
     assert np.array_equal(got.cpu().numpy(), wexp)
+    P.stream_release(s)
 
 
 def test_span_scratch_per_thread_streams(P):
