@@ -148,7 +148,9 @@ def test_span_stale_arrival_words_never_pair(P):
     exp = oracle.batch_csr(data, off)
     s = torch.cuda.Stream()  # (its own scratch: the epoch count starts here)
     torch.cuda.synchronize()
-    assert np.array_equal(u32(P.batch_csr(d, o, stream=s)), exp)
+    first = P.batch_csr(d, o, stream=s)
+    s.synchronize()
+    assert np.array_equal(u32(first), exp)
     calls = 1
     for value in (1, 2, 3, 5, 6, 7, (2 << 2) | 1, (3 << 2) | 2, (7 << 2) | 1, (9 << 2) | 2):
         rc = P.lib().lnl_diag_fill_span_arrivals(s.cuda_stream, value)
