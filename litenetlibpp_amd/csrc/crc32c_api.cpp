@@ -240,10 +240,14 @@ int csr_path() {
 // Bound.  At most LNL_STREAM_CACHE streams' scratch is kept per device and map;
 // beyond that the least recently used entry is freed.  Its stream may have
 // been destroyed, so the free goes on a library-owned stream of the device,
-// behind the entry's last use: every call records an event on its stream once
-// it has enqueued everything that reads the entry, and the eviction makes the
-// library stream wait for that event (no host or device-wide synchronise, and
-// a caller in stream capture is not disturbed by another stream's eviction).
+// behind the entry's last use: once more than half the bound is in use on the
+// device, every call records an event on its stream when it has enqueued
+// everything that reads the entry, and the eviction makes the library stream
+// wait for that event (no host or device-wide synchronise, and a caller in
+// stream capture is not disturbed by another stream's eviction).  Below half
+// the bound no event is recorded: an event record costs 3-5 us a call (round
+// 5 A/B, DESIGN round-5 table), and a victim whose last call recorded none -- its stream
+// went idle while the cache was small -- is freed after a device synchronise.
 // lnl_stream_release frees a stream's entries explicitly, stream-ordered.
 // A call holds the cache's mutex from its choice of the entry until that event
 // is recorded, so an entry is never evicted or released between a call's
@@ -266,12 +270,25 @@ StreamKey stream_key(hipStream_t st) {
     return k;
 }
 
+#ifndef LNL_SCRATCH_EVENTS
+#define LNL_SCRATCH_EVENTS 1  // 0 (experiments): never record the last-use event
+#endif
+// The last-use event only orders a free on the library stream of the same device
+#ifndef LNL_SCRATCH_EVENT_FLAGS
+#define LNL_SCRATCH_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
+#ifndef LNL_SCRATCH_EVENT_FROM
+#define LNL_SCRATCH_EVENT_FROM (LNL_STREAM_CACHE / 2)  // entries on the device before calls record events
+#endif
+
 struct SpanScratch {
     uint32_t* buf = nullptr;
     size_t words = 0;
     uint64_t calls = 0;          // span path: calls made on it (the control block parity and the exchange epoch)
     uint64_t used = 0;           // LRU tick
-    hipEvent_t done = nullptr;   // recorded after the last call's launches that read buf
+    hipEvent_t done = nullptr;   // recorded after the last call's launches that read buf, when `fence`
+    bool fence = false;          // this call records `done` (the cache is past LNL_SCRATCH_EVENT_FROM)
+    bool fenced = false;         // the last call did record it
 };
 
 // the library's own stream on the current device (evictions free on it)
@@ -299,8 +316,11 @@ struct ScratchCache {
         const StreamKey key = stream_key(st);
         SpanScratch& s = m[key];
         s.used = ++tick;
-        if (!s.done) {
-            hipError_t e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        size_t on_dev = 0;
+        for (auto& kv : m) on_dev += kv.first.dev == key.dev;
+        s.fence = LNL_SCRATCH_EVENTS && on_dev > (size_t)LNL_SCRATCH_EVENT_FROM;
+        if (s.fence && !s.done) {
+            hipError_t e = hipEventCreateWithFlags(&s.done, LNL_SCRATCH_EVENT_FLAGS);
             if (e != hipSuccess) {
                 s.done = nullptr;
                 return hip_fail(e, "hipEventCreate");
@@ -325,7 +345,8 @@ struct ScratchCache {
 
     // a call's launches that read the entry are enqueued on st.  Caller holds mu.
     static void used_by(SpanScratch* s, hipStream_t st) {
-        if (s && s->done) (void)hipEventRecord(s->done, st);
+        if (!s) return;
+        s->fenced = s->fence && s->done && hipEventRecord(s->done, st) == hipSuccess;
     }
 
     void evict(const StreamKey& keep) {
@@ -339,17 +360,17 @@ struct ScratchCache {
                 victim = it;
         }
         if (victim == m.end()) return;
-        // its stream may be gone: free on the library stream, behind its last use
+        // its stream may be gone: free on the library stream, behind its last
+        // use (its event, or a device synchronise when its last call recorded none)
         hipStream_t ls = library_stream(keep.dev);
         SpanScratch& v = victim->second;
-        if (ls && v.done) (void)hipStreamWaitEvent(ls, v.done, 0);
+        if (!v.fenced || !ls) (void)hipDeviceSynchronize();
+        else (void)hipStreamWaitEvent(ls, v.done, 0);
         if (v.buf) {
             if (ls)
                 (void)hipFreeAsync(v.buf, ls);
-            else {
-                if (v.done) (void)hipEventSynchronize(v.done);
+            else
                 (void)hipFree(v.buf);
-            }
         }
         if (v.done) (void)hipEventDestroy(v.done);
         m.erase(victim);

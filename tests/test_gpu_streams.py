@@ -233,3 +233,25 @@ def test_stream_release_and_cache_bound(P):
         P.stream_release(s)
     # releasing a stream the library never saw is a no-op
     assert P.lib().lnl_stream_release(torch.cuda.Stream().cuda_stream) == 0
+
+
+def test_cache_bound_with_calls_in_flight(P):
+    """Evictions while the victims' calls are still queued: 40 streams, three
+    rounds of calls with no host synchronise between them.  Past half the bound
+    each call records its last-use event and an eviction frees behind it on the
+    library stream; earlier entries are freed after a device synchronise."""
+    data, off = csr_batch(951, 60_000)
+    d, o = dev(data), dev(off.view(np.int64), torch.int64)
+    exp = oracle.batch_csr(data, off)
+    streams = [torch.cuda.Stream() for _ in range(40)]
+    outs = []
+    for rep in range(3):
+        for s in streams:
+            with torch.cuda.stream(s):
+                outs.append(P.batch_csr(d, o, stream=s))
+    torch.cuda.synchronize()
+    for out in outs:
+        assert np.array_equal(u32(out), exp)
+    for s in streams:
+        P.stream_release(s)
+    torch.cuda.synchronize()

@@ -44,6 +44,9 @@ VARIANTS = {
     "span_r3_tl": "-DLNL_SPAN_ROWS_LATE=0 -DLNL_SPAN_FOLD_MASK=0 -DLNL_SPAN_TAIL_REG=0 -DLNL_SPAN_DIAG=16",
     "run512": "-DLNL_RUN_THREADS=512",              # lane-run kernel: one 512-thread workgroup per CU
     "run512p": "-DLNL_RUN_THREADS=512 -DLNL_RUN_PRIO=1",  # ... with progress-based issue priority
+    "noevent": "-DLNL_SCRATCH_EVENTS=0",            # no per-call last-use event on the span / XOR scratch (round 4)
+    "ev_always": "-DLNL_SCRATCH_EVENT_FROM=0",      # every call records the last-use event (round 5's first form)
+    "ev_sys": "-DLNL_SCRATCH_EVENT_FROM=0 -DLNL_SCRATCH_EVENT_FLAGS=hipEventDisableTiming",  # ... with the system fence
     "app_u1": "-DLNL_APPEND_COPY_U=1",              # outbound layer: round 3's copy kernel (one chunk load in flight per lane)
     "app_u2": "-DLNL_APPEND_COPY_U=2",
     "app_u4": "-DLNL_APPEND_COPY_U=4",
