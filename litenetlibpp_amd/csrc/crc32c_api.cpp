@@ -1177,15 +1177,15 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
 #if LNL_EXPERIMENTS
     static const int flat_v = [] {
         const char* e = getenv("LNL_XOR_FLAT");  // 0: per-datagram kernel
-        return e ? atoi(e) : 6;
+        return e ? atoi(e) : 12;
     }();
     static const int flat_wg = [] {
         const char* e = getenv("LNL_XOR_FLAT_WG");  // workgroups per CU
         return e ? std::max(1, atoi(e)) : 8;
     }();
 #else
-    constexpr int flat_v = 6;   // 2 pieces in flight, nontemporal
-    constexpr int flat_wg = 8;  // workgroups per CU
+    constexpr int flat_v = 12;  // tiles of 2 x 256 pieces, nontemporal
+    constexpr int flat_wg = 8;  // workgroups per CU (persistent forms)
 #endif
     const bool flat_on = flat_v > 0;
     const uint64_t span = d_off ? 0 : (uint64_t)(n - 1) * stride + len;
@@ -1201,8 +1201,13 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
         f.n = n;
         f.SK = f.S % f.K;
         const uint32_t per = 256u * 4u;  // pieces per workgroup per step (kThreads x kUnroll)
-        const uint32_t grid = std::max(1u, std::min((f.pieces + per - 1) / per, (uint32_t)S->cus * (uint32_t)flat_wg));
-        const uint64_t step = 16ull * grid * 256u;
+        uint32_t grid = std::max(1u, std::min((f.pieces + per - 1) / per, (uint32_t)S->cus * (uint32_t)flat_wg));
+        uint64_t step = 16ull * grid * 256u;
+        if (flat_v > 10) {  // tiles of tu x 256 pieces, one per workgroup, the grid in batch order
+            const uint32_t tu = flat_v == 11 || flat_v == 15 ? 1u : flat_v == 13 ? 4u : 2u;
+            grid = std::max(1u, (f.pieces + 256u * tu - 1u) / (256u * tu));
+            step = 16ull * 256u;
+        }
         f.sd = (uint32_t)(step / f.S);
         f.sr = (uint32_t)(step % f.S);
         f.srk = f.sr % f.K;
@@ -1218,12 +1223,25 @@ int xor_layer(uint8_t* d_base, const uint64_t* d_off, size_t stride, uint32_t le
 #ifndef LNL_XOR_CSR_FLAT
 #define LNL_XOR_CSR_FLAT 3
 #endif
+    // Grid: one workgroup per 32 datagrams, between 16 and 128 per CU (~3 chunks
+    // per wave on config 3; the bytes are on the device, so n sizes it).  More
+    // waves than a persistent 4 per CU keep the grid inside a narrower window
+    // of the batch (round 5).
 #ifndef LNL_XOR_GRID_WGS
-#define LNL_XOR_GRID_WGS 4  // workgroups per CU (112 VGPRs: 4 waves per SIMD)
+#define LNL_XOR_GRID_WGS 128u  // workgroups per CU, at most
+#endif
+#ifndef LNL_XOR_GRID_MIN
+#define LNL_XOR_GRID_MIN 16u  // workgroups per CU, at least
+#endif
+#ifndef LNL_XOR_GRID_PER
+#define LNL_XOR_GRID_PER 32u  // datagrams per workgroup (0: always LNL_XOR_GRID_WGS per CU)
 #endif
     if (LNL_XOR_CSR_FLAT == 3 && d_off) {
+        const uint32_t lo = (uint32_t)S->cus * LNL_XOR_GRID_MIN, hi = (uint32_t)S->cus * LNL_XOR_GRID_WGS;
+        const uint32_t want = LNL_XOR_GRID_PER ? (n + LNL_XOR_GRID_PER - 1u) / LNL_XOR_GRID_PER : hi;
+        const int grid = (int)std::min(hi, std::max(lo, want));
         return with_xor_map((hipStream_t)hip_stream, (size_t)n + 1u, [&](uint32_t* map) {
-            hipError_t e = lnl::launch_xor_csr_grid(a, map, n + 1u, S->cus * LNL_XOR_GRID_WGS, (hipStream_t)hip_stream);
+            hipError_t e = lnl::launch_xor_csr_grid(a, map, n + 1u, grid, (hipStream_t)hip_stream);
             return e == hipSuccess ? 0 : hip_fail(e, "xor csr grid launch");
         });
     }

@@ -11,7 +11,7 @@
 // share chunks with the neighbouring datagrams, go one byte per lane.  Each
 // lane issues the loads of up to kCopyU chunks before it stores any (round 3
 // issued one, then stored it: one memory round trip per 512 bytes of a
-// datagram).  ~50 VGPRs, 8 waves per SIMD.
+// datagram).  ~50 VGPRs, 8 waves per SIMD; one datagram per team (below).
 //
 // The one-pass form (the team computes each datagram's CRC from the registers
 // it copies) and the other round-4 copy shapes were built, parity-green and
@@ -112,12 +112,17 @@ __global__ __launch_bounds__(kCopyThreads) void append_copy_kernel(AppendArgs a)
 
 }  // namespace
 
+// Grid: one datagram per team, so the dispatcher hands out the burst in order
+// and the whole chip reads and writes inside one moving window of it.  A grid
+// capped at 16 workgroups per CU, teams striding over the datagrams, took
+// 462 us per config-3 call against 432 (round 5): strided teams
+// drift apart and spread the reads and writes over more DRAM pages.
 #ifndef LNL_APPEND_WGS
-#define LNL_APPEND_WGS 16u  // copy kernel: workgroups per CU (teams stride over the datagrams)
+#define LNL_APPEND_WGS 0u  // workgroups per CU (0: no cap; experiments: a strided, persistent grid)
 #endif
 hipError_t launch_append(const AppendArgs& a, int cus, hipStream_t stream) {
     const uint32_t per = kCopyThreads / kAppTeam;
-    const uint32_t want = (a.n + per - 1) / per, cap = (uint32_t)cus * LNL_APPEND_WGS;
+    const uint32_t want = (a.n + per - 1) / per, cap = LNL_APPEND_WGS ? (uint32_t)cus * LNL_APPEND_WGS : 0xFFFFFFFFu;
     hipLaunchKernelGGL(append_copy_kernel, dim3(want < cap ? (want ? want : 1) : cap), dim3(kCopyThreads), 0, stream, a);
     return hipGetLastError();
 }

@@ -207,13 +207,16 @@ __device__ inline u32x4 flat_key(const uint32_t (*ks)[kKeyWords], const FlatArgs
     return k;
 }
 
-template <int kU, bool kNT>
+// kTile: workgroup b takes the kU x 256 consecutive pieces from b x kU x 256 on
+// (one pass, grid sized to the batch: the dispatcher hands out the batch in
+// order); otherwise a persistent grid strides over it, kU pieces per lane per step
+template <int kU, bool kNT, bool kTile = false>
 __global__ __launch_bounds__(kThreads) void xor_flat_kernel(XorArgs a, FlatArgs f) {
     __shared__ uint32_t ks[4][kKeyWords];
     stage_key(a, ks);
     __syncthreads();
-    const uint32_t T = gridDim.x * kThreads;
-    const uint32_t k0 = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t T = kTile ? kThreads : gridDim.x * kThreads;
+    const uint32_t k0 = blockIdx.x * kThreads * (kTile ? kU : 1) + threadIdx.x;
     if (k0 >= f.pieces) return;
     FlatState st;
     {
@@ -254,6 +257,7 @@ __global__ __launch_bounds__(kThreads) void xor_flat_kernel(XorArgs a, FlatArgs 
                     bp[j] ^= (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
             }
         }
+        if (kTile) break;
     }
 }
 
@@ -629,7 +633,7 @@ __global__ __launch_bounds__(256) void xor_csr_stream_kernel(XorArgs a, uint64_t
 // numbered XCD-major, so neighbouring chunks -- which share offsets lines --
 // run under one L2.
 #ifndef LNL_XOR_GRID_U
-#define LNL_XOR_GRID_U 4  // pieces per lane and chunk (4 KiB chunks)
+#define LNL_XOR_GRID_U 2  // pieces per lane and chunk (2 KiB chunks)
 #endif
 constexpr uint32_t kGridU = LNL_XOR_GRID_U;
 constexpr uint32_t kGridChunk = 64u * kGridU * 16u;  // 2 KiB per wave and chunk
@@ -679,6 +683,20 @@ __global__ __launch_bounds__(256) void xor_csr_grid_kernel(XorArgs a, uint64_t M
     __shared__ uint32_t ks[4][kKeyWords];
     __shared__ u32x4 below[17];    // below[b]: bytes [0, b) of a piece
     __shared__ uint32_t neg[16];   // neg[b] = -b mod K: the phase that puts key[0] on byte b
+    const uint64_t ab = (uint64_t)((uintptr_t)a.base & 15u);  // buffer misalignment
+    uint8_t* const abase = a.base - ab;                       // 16-byte aligned
+    const uint64_t B0 = a.off[0] - a.off0 + ab, B1 = a.off[a.n] - a.off0 + ab;  // the batch, from abase
+    if (B1 <= B0) return;
+    const uint64_t S = B0 & ~(uint64_t)15;
+    const uint64_t chunks = (B1 - S + kGridChunk - 1u) / kGridChunk;
+#ifndef LNL_XOR_GRID_XCD
+#define LNL_XOR_GRID_XCD 0  // 1: waves numbered XCD-major (neighbouring chunks under one L2)
+#endif
+    const uint32_t G = gridDim.x;
+    const uint32_t vb = LNL_XOR_GRID_XCD && (G & 7u) == 0u ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    // (the grid is sized from n, not from the bytes: a workgroup past the
+    // batch's chunks leaves before it stages anything)
+    if ((uint64_t)vb * 4u >= chunks) return;
     stage_key(a, ks);
     const uint32_t K = a.key_len;
     if (threadIdx.x < 17u) {
@@ -694,16 +712,7 @@ __global__ __launch_bounds__(256) void xor_csr_grid_kernel(XorArgs a, uint64_t M
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t ab = (uint64_t)((uintptr_t)a.base & 15u);  // buffer misalignment
-    uint8_t* const abase = a.base - ab;                       // 16-byte aligned
-    const uint64_t B0 = a.off[0] - a.off0 + ab, B1 = a.off[a.n] - a.off0 + ab;  // the batch, from abase
-    if (B1 <= B0) return;
-    const uint64_t S = B0 & ~(uint64_t)15;
-    const uint64_t chunks = (B1 - S + kGridChunk - 1u) / kGridChunk;
     const uint32_t mk = map_shift(chunks, cap);  // chunk c's map word: first[c >> mk]
-    // XCD-major wave numbering (workgroup b runs on XCD b mod 8)
-    const uint32_t G = gridDim.x;
-    const uint32_t vb = (G & 7u) == 0u ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
     const uint64_t W = (uint64_t)G * 4u, gw = (uint64_t)vb * 4u + w;
     if (gw >= chunks) return;
     auto pos = [&](uint32_t d) -> uint64_t { return a.off[d] - a.off0 + ab; };
@@ -852,10 +861,15 @@ hipError_t launch_xor_csr_flat(const XorArgs& a, int grid, hipStream_t stream) {
 
 hipError_t launch_xor_flat(const XorArgs& a, const FlatArgs& f, int grid, int variant, hipStream_t stream) {
 #if !LNL_EXPERIMENTS
-    (void)variant;  // product: 2 pieces in flight per lane, nontemporal
-    hipLaunchKernelGGL((xor_flat_kernel<2, true>), dim3(grid), dim3(kThreads), 0, stream, a, f);
+    (void)variant;  // product: tiles of 2 x 256 pieces, nontemporal
+    hipLaunchKernelGGL((xor_flat_kernel<2, true, true>), dim3(grid), dim3(kThreads), 0, stream, a, f);
 #else
-    switch (variant) {  // pieces in flight per lane x cache policy (measured in DESIGN 4.8)
+    switch (variant) {  // pieces in flight per lane x cache policy (measured in DESIGN 4.8); 11..14: tiles
+        case 11: hipLaunchKernelGGL((xor_flat_kernel<1, true, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        case 12: hipLaunchKernelGGL((xor_flat_kernel<2, true, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        case 13: hipLaunchKernelGGL((xor_flat_kernel<4, true, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        case 14: hipLaunchKernelGGL((xor_flat_kernel<2, false, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
+        case 15: hipLaunchKernelGGL((xor_flat_kernel<1, false, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
         case 2: hipLaunchKernelGGL((xor_flat_kernel<4, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
         case 3: hipLaunchKernelGGL((xor_flat_kernel<8, false>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;
         case 4: hipLaunchKernelGGL((xor_flat_kernel<8, true>), dim3(grid), dim3(kThreads), 0, stream, a, f); break;

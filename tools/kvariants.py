@@ -47,10 +47,15 @@ VARIANTS = {
     "noevent": "-DLNL_SCRATCH_EVENTS=0",            # no per-call last-use event on the span / XOR scratch (round 4)
     "ev_always": "-DLNL_SCRATCH_EVENT_FROM=0",      # every call records the last-use event (round 5's first form)
     "ev_sys": "-DLNL_SCRATCH_EVENT_FROM=0 -DLNL_SCRATCH_EVENT_FLAGS=hipEventDisableTiming",  # ... with the system fence
+    "app_w16": "-DLNL_APPEND_WGS=16u",              # copy kernel: persistent grid, teams stride (round 4's product)
+    "xg_r4": "-DLNL_XOR_GRID_U=4 -DLNL_XOR_GRID_XCD=1 -DLNL_XOR_GRID_PER=0 -DLNL_XOR_GRID_WGS=4u",  # CSR XOR grid, round 4
+    "xg_xcd": "-DLNL_XOR_GRID_XCD=1",               # ... XCD-major wave numbering
+    "xg_per16": "-DLNL_XOR_GRID_PER=16u",           # ... one workgroup per 16 datagrams
+    "xg_per64": "-DLNL_XOR_GRID_PER=64u",
     "app_u1": "-DLNL_APPEND_COPY_U=1",              # outbound layer: round 3's copy kernel (one chunk load in flight per lane)
     "app_u2": "-DLNL_APPEND_COPY_U=2",
     "app_u4": "-DLNL_APPEND_COPY_U=4",
-    "app_w8": "-DLNL_APPEND_WGS=8u",                # copy kernel: workgroups per CU (default 16)
+    "app_w8": "-DLNL_APPEND_WGS=8u",                # copy kernel: workgroups per CU (default: no cap)
     "app_w32": "-DLNL_APPEND_WGS=32u",
     "fix64": "-DLNL_SPAN_FIX_WGS=64u",              # batch kernel after the span kernel: 64 workgroups
     "fix8": "-DLNL_SPAN_FIX_WGS=8u",                # ... 8 workgroups
@@ -219,15 +224,16 @@ def run(names, rounds, workloads):
             def call(L):
                 L.lnl_crc32c_append_csr_dev(data.data_ptr(), off.data_ptr(), n_pk, wire.data_ptr(), out.data_ptr(),
                                             s.cuda_stream)
-        elif wl[0] == "xorcsr":  # ("xorcsr", n): XOR layer in place over a config-3-shaped CSR batch
+        elif wl[0] == "xorcsr":  # ("xorcsr", n[, lmin, lmax]): XOR layer in place over a CSR batch (config 3: 64..1400)
             n_pk = wl[1]
-            lens = torch.randint(64, 1401, (n_pk,), device=dev, generator=g, dtype=torch.int64)
+            lmin, lmax = (wl[2], wl[3]) if len(wl) > 3 else (64, 1400)
+            lens = torch.randint(lmin, lmax + 1, (n_pk,), device=dev, generator=g, dtype=torch.int64)
             off = torch.zeros(n_pk + 1, dtype=torch.int64, device=dev)
             off[1:] = torch.cumsum(lens, 0)
             total = int(off[-1])
             data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
             algo = 2 * total + 8 * (n_pk + 1)
-            wkey = f"xorcsr{n_pk}"
+            wkey = f"xorcsr{n_pk}" + (f"x{lmin}-{lmax}" if len(wl) > 3 else "")
             key = b"LiteNetLibPP-bench-key"
             for L in libs.values():
                 L.lnl_xor_layer_csr_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
