@@ -489,8 +489,15 @@ int launch_csr(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st)
 
 // Lane-run plan for a fixed-stride batch (crc32c_run.hip): how many leading
 // datagrams the run kernel covers.  0 = use the batch kernel for all.
+// Runs of 4 datagrams per lane, one batch (64 runs) per wave and a grid that
+// is not capped at the resident waves: the dispatcher then hands out the
+// batches in memory order and the chip reads inside a narrower window of the
+// batch.  Round 5: config 2 227.4 against 230.5 us for runs of 8
+// on a capped grid, 4000-byte strides 159.7 against 202.5, 512-byte 179.8
+// against 222.2, 256-byte 189.3 against 200.5 (1404-byte strides 236.5
+// against 235.2).
 #ifndef LNL_RUN_K
-#define LNL_RUN_K 8
+#define LNL_RUN_K 4
 #endif
 uint32_t run_plan(size_t stride, uint32_t len, uint32_t n, lnl::RunArgs& r) {
 #if defined(LNL_NO_RUN)  // experiment builds only (tools/kvariants.py): batch kernel for everything
@@ -584,7 +591,12 @@ extern "C" int lnl_crc32c_batch_fixed_dev(const uint8_t* d_base, size_t stride, 
         r.base = d_base;
         r.out = d_out;
         r.fold = S->fold;
-        hipError_t e = lnl::launch_crc32c_run(r, grid_for_waves(*S, r.nb, lnl::kRunThreads), st);
+#ifndef LNL_RUN_UNCAPPED
+#define LNL_RUN_UNCAPPED 1  // one batch per wave, grid in batch order (0: capped at the resident waves)
+#endif
+        const int grid = LNL_RUN_UNCAPPED ? (int)((r.nb + lnl::kRunThreads / 64 - 1) / (lnl::kRunThreads / 64))
+                                          : grid_for_waves(*S, r.nb, lnl::kRunThreads);
+        hipError_t e = lnl::launch_crc32c_run(r, grid, st);
         if (e != hipSuccess) return hip_fail(e, "kernel launch");
         if (n_main == n) return 0;
     }

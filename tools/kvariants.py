@@ -90,7 +90,10 @@ VARIANTS = {
     "span_nob2": "-DLNL_SPAN_DIAG=64",              # ... a row's second and later boundaries skipped (wrong CRCs)
     "bucketed": ("", 4),                            # CSR: the bucketed batch kernel (previous default)
     "batch": "-DLNL_NO_RUN",                        # any-layout batch kernel for everything
-    "k4": "-DLNL_RUN_K=4",                          # lane runs of 4 / 16 datagrams
+    "k8c": "-DLNL_RUN_K=8 -DLNL_RUN_UNCAPPED=0",    # lane runs of 8, grid capped at the resident waves (round 4)
+    "k2u": "-DLNL_RUN_K=2",                         # lane runs of 2 (one batch per wave, uncapped: the default)
+    "k4c": "-DLNL_RUN_UNCAPPED=0",                  # lane runs of 4, capped grid
+    "k8": "-DLNL_RUN_K=8",                          # lane runs of 8 / 16 datagrams (uncapped grid)
     "k16": "-DLNL_RUN_K=16",
     "q32": "-DLNL_RUN_QMIN=32",                     # lane runs 32 datagrams apart (default: 16 at S = 1400)
     "q64": "-DLNL_RUN_QMIN=64",
