@@ -40,12 +40,18 @@ __device__ LNL_INLINE void store16(uint64_t a, uint32_t x, uint32_t y, uint32_t 
     asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(a), "v"(u32x4{x, y, z, w}) : "memory");
 }
 
-constexpr uint32_t kAppTeam = 32;  // lanes per datagram (16: 559, 32: 512, 64: 613 us in round 2)
+#ifndef LNL_APPEND_TEAM
+#define LNL_APPEND_TEAM 32u  // lanes per datagram (16: 559, 32: 512, 64: 613 us in round 2)
+#endif
+constexpr uint32_t kAppTeam = LNL_APPEND_TEAM;
 #ifndef LNL_APPEND_COPY_U
 #define LNL_APPEND_COPY_U 3  // chunk loads in flight per lane (1: round 3's kernel)
 #endif
 constexpr uint32_t kCopyU = LNL_APPEND_COPY_U;
-constexpr int kCopyThreads = 256;
+#ifndef LNL_APPEND_THREADS
+#define LNL_APPEND_THREADS 256
+#endif
+constexpr int kCopyThreads = LNL_APPEND_THREADS;
 __device__ inline uint8_t out_byte(uint64_t x, uint64_t P1, uint64_t delta, uint32_t crc) {
     return x < P1 ? *LNL_G(const uint8_t, x - delta) : (uint8_t)(crc >> (8u * (uint32_t)(x - P1)));
 }
@@ -93,8 +99,13 @@ __global__ __launch_bounds__(kCopyThreads) void append_copy_kernel(AppendArgs a)
                 const uint64_t w = wb + 16ull * kAppTeam * u;
                 if (w < c1) {
                     const uint64_t sw = (w - delta) & ~(uint64_t)3;
+#if defined(LNL_APPEND_DIAG) && (LNL_APPEND_DIAG & 2)  // (diagnostic build: chunk loads aligned, no 5th dword)
+                    v[u] = *LNL_G(const U4a, sw & ~(uint64_t)15);
+                    v4[u] = 0u;
+#else
                     v[u] = *LNL_G(const U4a, sw);
                     v4[u] = c ? *LNL_G(const uint32_t, sw + 16) : 0u;  // (byte w - delta + 15: inside the payload)
+#endif
                 }
             }
 #pragma unroll
@@ -105,8 +116,10 @@ __global__ __launch_bounds__(kCopyThreads) void append_copy_kernel(AppendArgs a)
                             __builtin_amdgcn_alignbyte(v[u].w, v[u].z, c), __builtin_amdgcn_alignbyte(v4[u], v[u].w, c));
             }
         }
+#if !(defined(LNL_APPEND_DIAG) && (LNL_APPEND_DIAG & 1))  // (diagnostic build: no head / tail byte stores)
         if (b0) *LNL_G(uint8_t, x0) = v0;
         if (b1) *LNL_G(uint8_t, x1) = v1;
+#endif
     }
 }
 

@@ -47,6 +47,18 @@ VARIANTS = {
     "noevent": "-DLNL_SCRATCH_EVENTS=0",            # no per-call last-use event on the span / XOR scratch (round 4)
     "ev_always": "-DLNL_SCRATCH_EVENT_FROM=0",      # every call records the last-use event (round 5's first form)
     "ev_sys": "-DLNL_SCRATCH_EVENT_FROM=0 -DLNL_SCRATCH_EVENT_FLAGS=hipEventDisableTiming",  # ... with the system fence
+    "app_nobyte": "-DLNL_APPEND_DIAG=1",            # diagnostic (wrong wire): no head / tail byte stores
+    "app_aligned": "-DLNL_APPEND_DIAG=2",           # diagnostic (wrong wire): aligned chunk loads only
+    "app_diag3": "-DLNL_APPEND_DIAG=3",             # both
+    "app_t16": "-DLNL_APPEND_TEAM=16u",             # copy kernel: 16 lanes per datagram (3 chunks in flight each)
+    "app_t16u4": "-DLNL_APPEND_TEAM=16u -DLNL_APPEND_COPY_U=4",
+    "app_t16u6": "-DLNL_APPEND_TEAM=16u -DLNL_APPEND_COPY_U=6",
+    "app_t8u12": "-DLNL_APPEND_TEAM=8u -DLNL_APPEND_COPY_U=12",
+    "app_t32u6": "-DLNL_APPEND_COPY_U=6",
+    "app_t64u2": "-DLNL_APPEND_TEAM=64u -DLNL_APPEND_COPY_U=2",
+    "app_t64u1": "-DLNL_APPEND_TEAM=64u -DLNL_APPEND_COPY_U=1",
+    "app_th512": "-DLNL_APPEND_THREADS=512",        # ... 512-thread workgroups
+    "app_th128": "-DLNL_APPEND_THREADS=128",
     "app_w16": "-DLNL_APPEND_WGS=16u",              # copy kernel: persistent grid, teams stride (round 4's product)
     "xg_r4": "-DLNL_XOR_GRID_U=4 -DLNL_XOR_GRID_XCD=1 -DLNL_XOR_GRID_PER=0 -DLNL_XOR_GRID_WGS=4u",  # CSR XOR grid, round 4
     "xg_xcd": "-DLNL_XOR_GRID_XCD=1",               # ... XCD-major wave numbering
@@ -77,6 +89,8 @@ VARIANTS = {
     "xgrid_dflt": "-DLNL_XOR_CSR_NT=0",             # ... default cache policy
     "xcsr_prev": "",                                # A/B slot: built from another lnl_xor.hip copied in by hand             # CSR XOR: the per-datagram kernel (before)
     "span_r2": "-DLNL_SPAN_ROUNDS=2u",              # CSR span: segments for two wave-batches per wave (static)
+    "span_r3": "-DLNL_SPAN_ROUNDS=3u",
+    "span_r4": "-DLNL_SPAN_ROUNDS=4u",
     "disp_scan": "-DLNL_DISPATCH_SCAN=1",           # dispatch passes with the hipCUB scan between them (before: product sums workgroup totals)
     "walk_norow": "-DLNL_WALK_DIAG=1",              # filter + dispatch: no per-row walk (wrong packets)
     "walk_noend": "-DLNL_WALK_DIAG=2",              # ... no walk at datagram ends (wrong packets)
