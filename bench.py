@@ -305,6 +305,32 @@ def hbm_probe_peak(data, device):
     return best
 
 
+def hbm_probe_sectors(data, device, n=1 << 22):
+    """Measured rate of independent one-dword reads at n distinct random 64-B
+    sectors of the same buffer (hbm_probe.hip sector_read): the ceiling of a
+    walk that touches one sector per dependent read, in 64-B sectors' GB/s."""
+    so = os.path.join(ROOT, "litenetlibpp_amd", "libhbm_probe.so")
+    if not os.path.exists(so):
+        return None
+    L = ctypes.CDLL(so)
+    L.lnl_probe_sector_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+    L.lnl_probe_sector_read.restype = ctypes.c_int64
+    sink = torch.zeros(4, dtype=torch.int32, device=device)
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        if L.lnl_probe_sector_read(data.data_ptr(), data.numel(), n, 1, sink.data_ptr(), s.cuda_stream) <= 0:
+            return None
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        L.lnl_probe_sector_read(data.data_ptr(), data.numel(), n, 1, sink.data_ptr(), s.cuda_stream)
+    e1.record()
+    torch.cuda.synchronize()
+    return 64.0 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+
 def cpu_quota() -> int | None:
     """CPUs the cgroup grants this process (cpu.max quota / period), if capped.
     On the GPU box os.cpu_count() and the affinity mask show the whole machine
@@ -654,6 +680,11 @@ def main():
             line["roofline"]["sector_granular_frac"] = round(lb / HBM_PEAK_GBS, 4)
             if traffic:  # (the walk's FETCH_SIZE factor is calibrated: profiles/fetch_calibration.json)
                 line["roofline"]["traffic_over_sector_floor"] = round(traffic / w["line_bytes"], 3)
+            if not DRY:
+                sec = hbm_probe_sectors(w["data"], device)
+                if sec:
+                    line["roofline"]["measured_random_sector_gbs"] = round(sec, 1)
+                    line["roofline"]["sector_frac_of_measured"] = round(lb / sec, 4)
         if not DRY:
             probe = hbm_probe_peak(w["data"], device)
             if probe:
