@@ -258,6 +258,42 @@ def run(names, rounds, workloads):
 
             def call(L):
                 L.lnl_xor_layer_csr_dev(data.data_ptr(), off.data_ptr(), n_pk, key, len(key), s.cuda_stream)
+        elif wl[0] == "disp":  # ("disp", n): lnl_dispatch_csr_dev over n MERGED containers of 5 x 256-B packets
+            n_pk = wl[1]
+            S = 1 + 5 * 259 + 4
+            data = torch.randint(0, 256, (n_pk * S,), dtype=torch.uint8, device=dev, generator=g)
+            d2 = data.view(n_pk, S)
+            d2[:, 0] = 0x0C
+            for j in range(5):
+                d2[:, 1 + 259 * j] = 1
+                d2[:, 2 + 259 * j] = 1
+                d2[:, 3 + 259 * j] = 0
+            off = torch.arange(0, (n_pk + 1) * S, S, dtype=torch.int64, device=dev)
+            st = torch.ones(n_pk, dtype=torch.uint8, device=dev)  # every container accepted
+            k = 5 * n_pk
+            pst = torch.empty(k, dtype=torch.int64, device=dev)
+            pl = torch.empty(k, dtype=torch.int32, device=dev)
+            pp = torch.empty(k, dtype=torch.int32, device=dev)
+            tot = torch.zeros(1, dtype=torch.int32, device=dev)
+            algo = n_pk * 10 + 19 * k
+            wkey = f"disp{n_pk}"
+            outs_ref = {}
+
+            def call(L):
+                L.lnl_dispatch_csr_dev(
+                    ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), ctypes.c_uint32(n_pk),
+                    ctypes.c_void_p(st.data_ptr()), ctypes.c_void_p(pst.data_ptr()), ctypes.c_void_p(pl.data_ptr()),
+                    ctypes.c_void_p(pp.data_ptr()), ctypes.c_uint32(k), ctypes.c_void_p(tot.data_ptr()),
+                    ctypes.c_void_p(s.cuda_stream))
+            for name, L in libs.items():  # same packets from every variant
+                pst.fill_(-1)
+                call(L)
+                torch.cuda.synchronize()
+                outs_ref[name] = (int(tot.item()), pst.clone(), pl.clone(), pp.clone())
+            ref0 = next(iter(outs_ref.values()))
+            for name, r in outs_ref.items():
+                same = r[0] == ref0[0] and all(torch.equal(x, y) for x, y in zip(r[1:], ref0[1:]))
+                print(f"{name}@{wkey} packets {r[0]} same-as-first {same}", flush=True)
         elif wl[0] == "fd":  # ("fd", n): filter + dispatch over n MERGED containers of 5 x 256-B packets
             n_pk = wl[1]
             S = 1 + 5 * 259 + 4
@@ -334,7 +370,7 @@ def main():
     if a.cmd == "build":
         build(names)
     else:
-        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.split(":")[0] in ("csr", "xor", "append", "filter", "fd", "xorcsr")
+        wl = [(w.split(":")[0],) + tuple(int(v) for v in w.split(":")[1:]) if w.split(":")[0] in ("csr", "xor", "append", "filter", "fd", "xorcsr", "disp")
               else tuple(int(v) for v in w.split(":")) for w in a.workloads.split(",")]
         res = run(names, a.rounds, wl)
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
