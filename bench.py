@@ -271,7 +271,8 @@ def hbm_probe_peak(data, device):
     plain streams (global_load_dwordx4 nt, LDS-DMA nt) over the whole buffer;
     forms 2-4 read it in the shape of a segment-per-lane CSR kernel (48-line
     segments, one round of every resident wave: per-lane lines into VGPRs with
-    the default / nt policy, and by LDS-DMA)."""
+    the default / nt policy, and by LDS-DMA); forms 11-13 are plain streams on
+    one-shot grids handed out in buffer order."""
     so = os.path.join(ROOT, "litenetlibpp_amd", "libhbm_probe.so")
     if not os.path.exists(so):
         return None
@@ -285,8 +286,8 @@ def hbm_probe_peak(data, device):
     seg_round = cus * 8 * 64 * 48 * 128
     best = {}
     waves = {5: 5, 6: 6}
-    for form in (0, 1, 2, 3, 4, 5, 6, 7):
-        nbytes = data.numel() // 8192 * 8192 if form < 2 else seg_round * waves.get(form, 8) // 8
+    for form in (0, 1, 2, 3, 4, 5, 6, 7, 11, 12, 13):
+        nbytes = data.numel() // 8192 * 8192 if form < 2 or form > 10 else seg_round * waves.get(form, 8) // 8
         if nbytes > data.numel() or nbytes == 0:
             continue
         rc = 0
@@ -688,12 +689,15 @@ def main():
         if not DRY:
             probe = hbm_probe_peak(w["data"], device)
             if probe:
-                peak = max(probe[0], probe[1])
+                peak = max(v for k, v in probe.items() if k in (0, 1, 11, 12, 13))  # whole-buffer streams
                 names = {0: "global_load_dwordx4 nt", 1: "global_load_lds_dwordx4 nt",
                          2: "segment lanes, VGPR loads", 3: "segment lanes, VGPR loads nt",
                          4: "segment lanes, LDS-DMA nt", 5: "segment lanes, LDS-DMA nt, 5 waves/CU",
                          6: "segment lanes, LDS-DMA nt, 6 waves/CU",
-                         7: "segment lanes, VGPR-staged nt + LDS transpose"}
+                         7: "segment lanes, VGPR-staged nt + LDS transpose",
+                         11: "one-shot grid, 4 KiB per workgroup, dwordx4 nt",
+                         12: "one-shot grid, 16 KiB per workgroup, dwordx4 nt",
+                         13: "one-shot grid, 8 KiB per wave, LDS-DMA nt"}
                 line["roofline"]["measured_stream_read_peak_gbs"] = round(peak, 1)
                 line["roofline"]["measured_stream_read_forms_gbs"] = {names[k]: round(v, 1) for k, v in probe.items()}
                 line["roofline"]["frac_of_measured_peak"] = round(achieved / peak, 4)
