@@ -166,10 +166,15 @@ int grid_for_waves(const DeviceState& S, uint32_t waves, int threads = lnl::kBlo
     return (int)std::max(1u, std::min(wgs, cap));
 }
 
+#ifndef LNL_BATCH_UNCAPPED
+#define LNL_BATCH_UNCAPPED 0  // experiments: batch kernel grid not capped at the resident waves
+#endif
 int launch(const DeviceState& S, lnl::BatchArgs a, int mode, hipStream_t st, uint32_t max_wgs = 0xFFFFFFFFu) {
     a.dummy = S.dummy;
     a.fold = S.fold;
-    const int grid = std::min(grid_for_waves(S, (a.n + 63u) / 64u), (int)std::min(max_wgs, 0x7FFFFFFFu));
+    const uint32_t bw = (a.n + 63u) / 64u, per = (uint32_t)lnl::kBlockThreads / 64u;
+    const int want = LNL_BATCH_UNCAPPED ? (int)std::max(1u, (bw + per - 1u) / per) : grid_for_waves(S, bw);
+    const int grid = std::min(want, (int)std::min(max_wgs, 0x7FFFFFFFu));
     hipError_t e = lnl::launch_crc32c_batch(a, mode, std::max(grid, 1), st);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     return 0;

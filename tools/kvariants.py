@@ -104,6 +104,7 @@ VARIANTS = {
     "span_nob2": "-DLNL_SPAN_DIAG=64",              # ... a row's second and later boundaries skipped (wrong CRCs)
     "bucketed": ("", 4),                            # CSR: the bucketed batch kernel (previous default)
     "batch": "-DLNL_NO_RUN",                        # any-layout batch kernel for everything
+    "bat_u": "-DLNL_BATCH_UNCAPPED=1",              # batch kernel: one batch per wave, grid in batch order
     "k8c": "-DLNL_RUN_K=8 -DLNL_RUN_UNCAPPED=0",    # lane runs of 8, grid capped at the resident waves (round 4)
     "k2u": "-DLNL_RUN_K=2",                         # lane runs of 2 (one batch per wave, uncapped: the default)
     "k4c": "-DLNL_RUN_UNCAPPED=0",                  # lane runs of 4, capped grid
