@@ -334,7 +334,10 @@ int lnl_crc32c_append_host_ex(const uint8_t* h_payload, const uint64_t* h_off, u
  * current device (the CSR span path's control and exchange blocks, the XOR
  * chunk map), stream-ordered.  Call it before destroying a stream the batch
  * entry points were given; the library also bounds what it keeps (the least
- * recently used streams' scratch is freed beyond LNL_STREAM_CACHE per device).
+ * recently used streams' scratch is freed beyond LNL_STREAM_CACHE per device,
+ * stream-ordered behind its last use; an entry last used while at most
+ * LNL_STREAM_CACHE / 2 streams held scratch is freed after a device
+ * synchronise).
  * Returns 0 (also when nothing was kept for the stream). */
 #define LNL_STREAM_CACHE 32
 int lnl_stream_release(void* hip_stream);
