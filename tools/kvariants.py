@@ -331,6 +331,17 @@ def run(names, rounds, workloads):
 
             def call(L):
                 L.lnl_crc32c_batch_fixed_dev(data.data_ptr(), stride, L_pk, n_pk, out.data_ptr(), s.cuda_stream)
+        if wl[0] in ("csr", "append") or isinstance(wl[0], int):
+            # outputs of every variant against the first (CRC workloads; the
+            # diagnostic builds are expected to differ)
+            ref_out = None
+            for n in names:
+                out.fill_(0)
+                call(libs[n])
+                torch.cuda.synchronize()
+                if ref_out is None:
+                    ref_out = out.clone()
+                print(f"{n}@{wkey} outputs same-as-first {bool(torch.equal(out, ref_out))}", flush=True)
         times = {n: [] for n in names}
         import time as _time
         t_settle = _time.perf_counter() + 0.15  # sustained clocks first (bench.py --settle-ms)
