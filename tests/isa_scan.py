@@ -164,6 +164,18 @@ def _blocks(insns):
     return blocks, succ
 
 
+_VREG_ONE = re.compile(r"v(\d+)")
+_VREG_RANGE = re.compile(r"\bv\[(\d+):(\d+)\]")
+
+
+def _vregs(text: str):
+    out = set()
+    for lo, hi in _VREG_RANGE.findall(text):
+        out |= set(range(int(lo), int(hi) + 1))
+    out |= {int(i) for i in re.findall(r"\bv(\d+)\b", _VREG_RANGE.sub(" ", text))}
+    return out
+
+
 _SREG_RANGE = re.compile(r"\bs\[(\d+):(\d+)\]")
 _SREG_ONE = re.compile(r"\bs(\d+)\b")
 # scalar instructions without a scalar destination operand
@@ -190,6 +202,17 @@ def _imm(text: str):
         return int(text.strip(), 0)
     except ValueError:
         return None
+
+
+def _cmp_ints(c: str, t: str, a: int, b: int) -> bool:
+    """s_cmp_<c>_<t> of two known values."""
+    bits = 64 if t.endswith("64") else 32
+    mask = (1 << bits) - 1
+    a, b = a & mask, b & mask
+    if t.startswith("i"):
+        a = a - (1 << bits) if a >> (bits - 1) else a
+        b = b - (1 << bits) if b >> (bits - 1) else b
+    return {"lt": a < b, "le": a <= b, "gt": a > b, "ge": a >= b, "eq": a == b, "lg": a != b}[c]
 
 
 def _cmp_expr(op: str, a: str, b: str):
@@ -294,25 +317,37 @@ class Scalar:
     with s_and / s_or / s_andn2, s_and(n2)_b64 vcc, exec, s[a:b] and
     s_cbranch_vcc(n)z / _scc0/1 on the same comparisons later -- so that the
     scan does not walk paths the kernel can never take."""
-    __slots__ = ("vals", "scc", "vcc", "facts")
+    __slots__ = ("vals", "scc", "vcc", "facts", "vv")
 
-    def __init__(self, vals=None, scc=None, vcc=None, facts=None):
+    def __init__(self, vals=None, scc=None, vcc=None, facts=None, vv=None):
         self.vals = vals or {}      # sgpr operand text -> int | formula
         self.scc = scc              # formula or None
         self.vcc = vcc              # formula or None
         self.facts = facts or {}    # comparison -> bool
+        self.vv = vv or {}          # vgpr -> formula: 1 in every lane where it holds, else 0
+                                    # (v_cndmask_b32 v, 0, 1, mask -- uni() of a flag)
 
     def key(self):
-        return (frozenset(self.vals.items()), self.scc, self.vcc, frozenset(self.facts.items()))
+        return (frozenset(self.vals.items()), self.scc, self.vcc, frozenset(self.facts.items()),
+                frozenset(self.vv.items()))
 
     def copy(self):
-        return Scalar(dict(self.vals), self.scc, self.vcc, dict(self.facts))
+        return Scalar(dict(self.vals), self.scc, self.vcc, dict(self.facts), dict(self.vv))
 
     def formula(self, operand):
-        """The operand as a mask formula, or None."""
+        """The operand as a mask formula, or None (a 32-bit half of a 64-bit
+        mask is all-ones or zero as the mask is: the same formula)."""
         if operand == "exec":
             return True
         v = self.vals.get(operand, _imm(operand) if _imm(operand) is not None else None)
+        if v is None:
+            m = _SREG_ONE.fullmatch(operand)
+            if m:
+                r = int(m.group(1))
+                for pair in (f"s[{r}:{r + 1}]", f"s[{r - 1}:{r}]"):
+                    w = self.vals.get(pair)
+                    if w is not None and not isinstance(w, int):
+                        return w
         if v is None:
             return None
         if isinstance(v, int):
@@ -347,6 +382,12 @@ class Scalar:
                 else:
                     self.vals[k] = g
         self.scc, self.vcc = fix(self.scc), fix(self.vcc)
+        for r, v in list(self.vv.items()):
+            g = fix(v)
+            if g is None:
+                del self.vv[r]
+            else:
+                self.vv[r] = g
         for e in [e for e in self.facts if _expr_regs(e) & regs]:
             del self.facts[e]
 
@@ -360,6 +401,15 @@ def _scalar_step(sc: Scalar, x: Insn):
     if op.startswith("s_"):
         m = _CMP.match(op)
         if m and len(ops) == 2:
+            known = [sc.vals.get(o) if isinstance(sc.vals.get(o), int) else _imm(o) for o in ops]
+            if known[0] is not None and known[1] is not None:  # two known values: the result
+                c.scc = _cmp_ints(m.group(1), m.group(2), known[0], known[1])
+                return [c]
+            if m.group(1) in ("eq", "lg") and 0 in known:  # a mask (or a copy of one) against zero
+                f = sc.formula(ops[1] if known[0] == 0 else ops[0])
+                if f is not None:
+                    c.scc = _not(f) if m.group(1) == "eq" else f
+                    return [c]
             e, truth = _cmp_expr(op, ops[0], ops[1])
             c.scc = ("cond", e) if truth else ("not", ("cond", e))
             return [c]
@@ -369,7 +419,17 @@ def _scalar_step(sc: Scalar, x: Insn):
             return [c]
         dst, src = ops[0], ops[1:]
         res = None  # the written mask's formula, for the logic ops
-        if op in ("s_and_b64", "s_or_b64", "s_andn2_b64", "s_orn2_b64", "s_xor_b64") and len(src) == 2:
+        if op in ("s_and_b32", "s_or_b32") and len(src) == 2:
+            # 32-bit logic on masks (or their halves): a nonzero immediate
+            # keeps the mask's truth (all-ones & imm != 0 exactly when it holds)
+            f, g = sc.formula(src[0]), sc.formula(src[1])
+            if f is None and g is not None and _imm(src[0]) not in (None, 0):
+                f = True
+            if g is None and f is not None and _imm(src[1]) not in (None, 0):
+                g = True
+            if f is not None and g is not None:
+                res = _and(f, g) if op == "s_and_b32" else _or(f, g)
+        elif op in ("s_and_b64", "s_or_b64", "s_andn2_b64", "s_orn2_b64", "s_xor_b64") and len(src) == 2:
             f, g = sc.formula(src[0]), sc.formula(src[1])
             if f is not None and g is not None:
                 if op == "s_and_b64":
@@ -400,6 +460,8 @@ def _scalar_step(sc: Scalar, x: Insn):
             c.vals[dst] = _imm(src[0])
         elif op.startswith("s_mov") and len(src) == 1 and src[0] in sc.vals:
             c.vals[dst] = sc.vals[src[0]]
+        elif op == "s_mov_b32" and len(src) == 1 and sc.formula(src[0]) not in (None, True, False):
+            c.vals[dst] = sc.formula(src[0])  # a half of a mask
         elif op in ("s_cselect_b64", "s_cselect_b32") and len(src) == 2 \
                 and _imm(src[0]) is not None and _imm(src[1]) is not None:
             a, b = _imm(src[0]), _imm(src[1])
@@ -416,10 +478,27 @@ def _scalar_step(sc: Scalar, x: Insn):
                     out.append(f)
                 return out
         return [c]
+    # VGPR flags: v_cndmask_b32 v, 0, 1, mask (the uniform 0 / 1 of a mask),
+    # read back by v_readfirstlane_b32 s, v; any other write of v forgets it
+    vdst = ops[0] if ops and op.startswith("v_") and not op.startswith(("v_cmp", "v_readlane", "v_readfirstlane")) \
+        else None
+    if vdst is not None:
+        for r in _vregs(vdst):
+            c.vv.pop(r, None)
+    elif ops and is_vmem(op) or op.startswith("ds_read"):
+        for r in (vmem_dest(x) if is_vmem(op) else _vregs(ops[0])):
+            c.vv.pop(r, None)
+    if op.startswith("v_cndmask_b32") and len(ops) == 4 and _imm(ops[1]) == 0 and _imm(ops[2]) == 1:
+        f = sc.formula(ops[3])
+        if f is not None and _VREG_ONE.fullmatch(ops[0]):
+            c.vv[int(ops[0][1:])] = f
     if "vcc" in x.args and not op.startswith("s_cbranch"):
         c.vcc = None  # (a VALU compare / carry writes it; reads do not matter)
     if op.startswith(("v_cmp", "v_readlane", "v_readfirstlane")) and ops:
         c.clobber(_sregs(ops[0]))
+        m = _VREG_ONE.fullmatch(ops[1]) if op.startswith("v_readfirstlane_b32") and len(ops) == 2 else None
+        if m and int(m.group(1)) in c.vv and _SREG_ONE.fullmatch(ops[0]):
+            c.vals[ops[0]] = c.vv[int(m.group(1))]
     return [c]
 
 
@@ -536,7 +615,7 @@ def scan_kernel(name: str, insns, max_consts: int = None) -> list:
         key = sc.key()
         if key not in seen[j] and len(seen[j]) >= cap:
             # widen: first the branch facts, then everything scalar
-            sc = Scalar(dict(sc.vals), sc.scc, sc.vcc)
+            sc = Scalar(dict(sc.vals), sc.scc, sc.vcc, None, dict(sc.vv))
             key = sc.key()
             if key not in seen[j] and len(seen[j]) >= 8 * cap:
                 sc = Scalar()
